@@ -1,0 +1,246 @@
+#!/usr/bin/env python3
+"""bench.py — FL encode+decode throughput on MI355X (BASELINE.json metric).
+
+One step = one pass of the hot path over one batch: FL encode of this rank's
+shard (per-frame width scan -> look-back offset scan -> bit-pack, one kernel),
+the multi-GPU size-scan (RCCL all-gather of {F_r, V_r} + exclusive scan; only
+when N > 1), and FL decode of the shard back to bytes. Inputs are resident in
+HBM before timing (device-generated, SURVEY.md §8(d) splitmix64 u8, seed 42,
+rank r holding global bytes [r*B, (r+1)*B) of one N*B-byte buffer), so `value`
+is whole-job input bytes / second through encode+decode, weak scaling.
+
+Default workload = BASELINE.json configs[1]: FL encode/decode of 1 GiB of
+uniform-random bytes per GPU, bit-exact against the reference fl-cpu (the
+1 GiB output's sha256 is the reference's).
+
+Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 under
+torch.distributed.run (one rank per GPU; backend nccl = RCCL over xGMI).
+"""
+from __future__ import annotations
+
+import argparse
+import hashlib
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "fl-rl-compression-mpi_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+import flrl  # noqa: E402
+from flrl.device import FLDevice, gen  # noqa: E402
+from flrl.dist import size_scan  # noqa: E402
+
+METRIC = ("encode+decode GB/s (input bytes) at 1/2/4/8 GPUs; % HBM roofline; "
+          "bit-exact round-trip")
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+GOLDEN_1GIB_U8_SHA = "0512b67cd1f3940885e5c3043c4541c5d8105403eb1273be20cd3c87d5ecef78"
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--bytes", type=int, default=1 << 30, help="input bytes per GPU")
+    p.add_argument("--kind", default="u8", choices=["u8", "lo4", "zero"])
+    p.add_argument("--seed", type=int, default=42)
+    p.add_argument("--cpu-sample", type=int, default=-1,
+                   help="bytes of the workload the CPU oracle times (default: min(bytes, 1 GiB)); 0 = skip")
+    p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"))
+    return p.parse_args()
+
+
+def file_sha(n, frames, bits: np.ndarray, values: np.ndarray) -> str:
+    h = hashlib.sha256()
+    h.update(np.array([n, frames, values.size], dtype="<u8").tobytes())
+    h.update(bits.tobytes())
+    h.update(values.tobytes())
+    return h.hexdigest()
+
+
+def cpu_baseline(kind: str, seed: int, sample: int, gpu_bits, gpu_values):
+    """Time the oracle (1 core, the reference fl-cpu's algorithm and loops) on
+    the first `sample` bytes of the same workload; also compare its output with
+    the GPU's for those bytes (128-aligned prefix => identical slices)."""
+    import oracle
+    a = oracle.gen(kind, sample, seed)
+    t0 = time.perf_counter()
+    bits, values = oracle.fl_compress(a)
+    t1 = time.perf_counter()
+    back = oracle.fl_decompress(sample, bits, values)
+    t2 = time.perf_counter()
+    ok = bool(np.array_equal(back, a))
+    same = None
+    if gpu_bits is not None and sample % 128 == 0:
+        same = bool(np.array_equal(gpu_bits[: bits.size], bits)
+                    and np.array_equal(gpu_values[: values.size], values))
+    return {
+        "value": round(sample / (t2 - t0) / 1e9, 4),
+        "unit": "GB/s",
+        "cores": 1,
+        "kind": "port",
+        "sample": f"{sample} bytes ({kind}, seed {seed}) = the first {sample} bytes of rank 0's "
+                  f"workload; oracle/flrl_oracle.c encode {t1 - t0:.2f} s + decode {t2 - t1:.2f} s, "
+                  f"single-threaded like the reference fl-cpu",
+        "encode_s": round(t1 - t0, 3),
+        "decode_s": round(t2 - t1, 3),
+        "roundtrip_ok": ok,
+        "gpu_bytes_equal_oracle": same,
+    }
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    n = args.bytes
+    assert n % 128 == 0, "per-GPU bytes must be frame-aligned for weak scaling"
+
+    x = gen(args.kind, n, args.seed, word_offset=rank * n // 8, device=dev)
+    codec = FLDevice(n, dev)
+    out = torch.empty_like(x)
+    stream = torch.cuda.current_stream()
+
+    # ---- correctness of this exact workload (outside the timed region) ----
+    codec.encode(x)
+    v = codec.values_size()
+    err = codec.error()
+    codec.decode(v, out=out)
+    err |= codec.error()
+    roundtrip = bool(torch.equal(out[:n], x[:n])) and err == 0
+    parity = {"roundtrip": roundtrip, "device_error": err}
+    gpu_bits = gpu_values = None
+    if rank == 0 and world == 1:
+        gpu_bits = codec.bits[: codec.frames].cpu().numpy()
+        gpu_values = codec.values[:v].cpu().numpy()
+        sha = file_sha(n, codec.frames, gpu_bits, gpu_values)
+        parity["fl_sha256"] = sha
+        if args.kind == "u8" and args.seed == 42 and n == 1 << 30:
+            parity["fl_sha256_matches_reference_fl_cpu"] = sha == GOLDEN_1GIB_U8_SHA
+
+    # ---- warmup ----
+    for _ in range(args.warmup):
+        codec.encode(x)
+        if world > 1:
+            size_scan(codec.sizes)
+        codec.decode(v, out=out)
+    torch.cuda.synchronize()
+
+    # ---- timed region: K steps ----
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        e = ev[k]
+        e[0].record(stream)
+        codec.encode(x)
+        e[1].record(stream)
+        if world > 1:
+            offs, totals = size_scan(codec.sizes)  # RCCL all-gather + exclusive scan
+        e[2].record(stream)
+        codec.decode(v, out=out)
+        e[3].record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    wall = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([wall], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        wall = float(t.item())
+    enc_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in ev]))
+    scan_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in ev]))
+    dec_ms = float(np.mean([e[2].elapsed_time(e[3]) for e in ev]))
+    assert codec.error() == 0
+
+    ms_per_step = wall * 1e3 / args.steps
+    value = world * n / (wall / args.steps) / 1e9
+
+    # algorithmic bytes per launch: encode N+F+V, decode F+V+N
+    alg = n + codec.frames + v
+    enc_gbs = alg / (enc_ms * 1e-3) / 1e9
+    dec_gbs = alg / (dec_ms * 1e-3) / 1e9
+    dominant = "fl_encode" if enc_ms >= dec_ms else "fl_decode"
+    achieved = enc_gbs if dominant == "fl_encode" else dec_gbs
+    traffic = None
+    try:
+        with open(args.traffic_json) as f:
+            tj = json.load(f)
+        if tj.get("bytes") == n and tj.get("kind") == args.kind:
+            traffic = tj["kernels"].get(dominant, {}).get("hbm_bytes_per_launch")
+    except (OSError, ValueError, KeyError):
+        traffic = None
+
+    if world > 1:
+        ok = torch.tensor([1 if parity["roundtrip"] else 0], device=dev)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        parity["roundtrip"] = bool(ok.item())
+
+    if rank == 0:
+        cpu = None
+        sample = min(n, 1 << 30) if args.cpu_sample < 0 else args.cpu_sample
+        if world == 1 and sample > 0:
+            cpu = cpu_baseline(args.kind, args.seed, sample, gpu_bits, gpu_values)
+        line = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "GB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": f"synthetic ({args.kind} splitmix64 seed {args.seed}, SURVEY.md §8(d), generated in HBM)",
+            "config": {
+                "workload": f"FL encode+decode of {n} {args.kind} bytes per GPU (BASELINE configs[1] at 1 GiB)",
+                "bytes_per_gpu": n,
+                "global_bytes": n * world,
+                "parallelism": f"dp{world}: 128-aligned shards, RCCL size-scan" if world > 1 else "single GPU",
+                "values_size_per_gpu": v,
+                "ratio": round((codec.frames + v + 24) / n, 6),
+            },
+            "roofline": {
+                "bound": "hbm",
+                "kernel": dominant,
+                "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": traffic,
+                "algorithmic_bytes_per_launch": alg,
+            },
+            "kernels": {
+                "fl_encode": {"ms": round(enc_ms, 4), "alg_GBps": round(enc_gbs, 1),
+                              "input_GBps": round(n / (enc_ms * 1e-3) / 1e9, 1)},
+                "fl_decode": {"ms": round(dec_ms, 4), "alg_GBps": round(dec_gbs, 1),
+                              "output_GBps": round(n / (dec_ms * 1e-3) / 1e9, 1)},
+                "size_scan": {"ms": round(scan_ms, 4)},
+            },
+            "cpu_baseline": cpu,
+            "parity": parity,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

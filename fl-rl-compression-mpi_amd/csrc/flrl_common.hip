@@ -1,0 +1,85 @@
+// flrl_common.hip — library plumbing (error strings, device query) and the
+// device-side synthetic input generator of SURVEY.md §8(d).
+#include <hip/hip_runtime.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include "flrl.h"
+#include "flrl_device.hpp"
+#include "flrl_internal.hpp"
+
+namespace flrl {
+
+static thread_local char g_err[512];
+
+int set_error(int code, const char *fmt, ...)
+{
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    va_end(ap);
+    return code;
+}
+
+void clear_error() { g_err[0] = 0; }
+
+// splitmix64 draw number w+1 from `seed` (counter form of SURVEY.md §8(d)).
+__device__ __forceinline__ uint64_t splitmix_at(uint64_t seed, uint64_t w)
+{
+    uint64_t z = seed + (w + 1) * 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+// Each thread writes 16 bytes = two 8-byte words per grid-stride step.
+__global__ __launch_bounds__(kThreads) void gen_kernel(uint32_t mask8, uint64_t seed,
+                                                       uint64_t word_offset, uint8_t *out,
+                                                       uint64_t n)
+{
+    const uint64_t mask = (uint64_t)mask8 * 0x0101010101010101ull;
+    const uint64_t stride = (uint64_t)gridDim.x * kThreads;
+    for (uint64_t t = (uint64_t)blockIdx.x * kThreads + threadIdx.x; t * 16 < n; t += stride) {
+        const uint64_t a = splitmix_at(seed, word_offset + 2 * t) & mask;
+        const uint64_t b = splitmix_at(seed, word_offset + 2 * t + 1) & mask;
+        const u32x4 v = u32x4{(uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32)};
+        store16_tail(out, t * 16, n, v);
+    }
+}
+
+}  // namespace flrl
+
+using namespace flrl;
+
+extern "C" const char *flrl_last_error(void) { return g_err; }
+
+extern "C" const char *flrl_version(void) { return "flrl 0.1.0 (gfx950)"; }
+
+extern "C" int flrl_device_count(void)
+{
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess)
+        return 0;
+    return n;
+}
+
+extern "C" int flrl_gen_device(int kind, uint64_t seed, uint64_t word_offset, uint8_t *d_out,
+                               size_t n, void *stream)
+{
+    if (kind < 0 || kind > 2)
+        return set_error(FLRL_E_ARG, "flrl_gen_device: kind %d is not counter-based (0-2)", kind);
+    if (n == 0)
+        return FLRL_OK;
+    if (!d_out || !aligned16(d_out))
+        return set_error(FLRL_E_ARG, "flrl_gen_device: output must be non-null, 16-B aligned");
+    const uint32_t mask8 = kind == 0 ? 0xFFu : (kind == 1 ? 0x0Fu : 0u);
+    const size_t threads_needed = div_up(n, 16);
+    const size_t blocks = threads_needed / kThreads + 1;
+    const uint32_t grid = (uint32_t)(blocks < 8192 ? blocks : 8192);
+    hipLaunchKernelGGL(gen_kernel, dim3(grid), dim3(kThreads), 0,
+                       static_cast<hipStream_t>(stream), mask8, seed, word_offset, d_out,
+                       (uint64_t)n);
+    FLRL_HIP(hipGetLastError());
+    return FLRL_OK;
+}

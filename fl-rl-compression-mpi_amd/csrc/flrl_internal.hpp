@@ -1,0 +1,47 @@
+// flrl_internal.hpp — host-side plumbing shared by the C-ABI translation units:
+// thread-local last-error string and HIP status checking that preserves the
+// message (the reference re-throws a sliced std::exception and loses it,
+// src/fl/fl_gpu.cu:296,401,419).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#include "flrl.h"
+
+namespace flrl {
+
+int set_error(int code, const char *fmt, ...);
+void clear_error();
+
+inline size_t div_up(size_t a, size_t b) { return (a + b - 1) / b; }
+inline size_t round_up(size_t a, size_t b) { return div_up(a, b) * b; }
+
+inline bool aligned16(const void *p) { return ((uintptr_t)p & 15u) == 0; }
+
+#define FLRL_HIP(expr)                                                                         \
+    do {                                                                                       \
+        hipError_t e_ = (expr);                                                                \
+        if (e_ != hipSuccess)                                                                  \
+            return ::flrl::set_error(FLRL_E_HIP, "%s failed: %s (%s:%d)", #expr,               \
+                                     hipGetErrorString(e_), __FILE__, __LINE__);                \
+    } while (0)
+
+// RAII device allocation for the synchronous host-buffer entry points.
+struct DevBuf {
+    void *p = nullptr;
+    ~DevBuf()
+    {
+        if (p)
+            (void)hipFree(p);
+    }
+    hipError_t alloc(size_t bytes) { return hipMalloc(&p, bytes ? bytes : 16); }
+    template <typename T>
+    T *as(size_t byte_off = 0) const
+    {
+        return reinterpret_cast<T *>(static_cast<uint8_t *>(p) + byte_off);
+    }
+};
+
+}  // namespace flrl

@@ -1,0 +1,300 @@
+"""flrl — Python binding of the MI355X FL/RL codec C ABI (include/flrl.h).
+
+The product is ``lib/libflrl.so`` (HIP kernels for gfx950 + host entry
+points); this module is a thin ctypes layer over it for tests and bench.py. It
+never falls back to a CPU implementation: if the library is missing, importing
+this module raises ImportError, and GPU entry points raise FLRLError when no HIP
+device is visible.
+
+Host-buffer API (mirrors the reference's FixedLength::gpuCompress /
+gpuDecompress, src/fl/fl_gpu.cuh:14-15):
+    fl_compress(data) -> FLCompressed(bits, values, input_size)
+    fl_decompress(input_size, bits, values) -> np.ndarray[uint8]
+    fl_compress_sharded(data, ngpus) -> FLCompressed   (gpuNCCLCompress, :16)
+    rl_compress(data) -> RLCompressed(counts, values, input_size)
+    rl_decompress(input_size, counts, values) -> np.ndarray[uint8]
+Device API (raw device pointers as ints; mirrors gpuCompressDevice, :17):
+    fl_encode_device / fl_decode_device / rl_encode_device / rl_decode_device,
+    gen_device, scratch_error, plus *_scratch_bytes sizing helpers.
+File formats: fl_file_bytes / parse_fl_file, rl_file_bytes / parse_rl_file.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import struct
+from dataclasses import dataclass
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+PKG_DIR = os.path.dirname(_HERE)
+LIB_PATH = os.path.join(PKG_DIR, "lib", "libflrl.so")
+CLI_PATH = os.path.join(PKG_DIR, "bin", "compress")
+HEADER_PATH = os.path.join(os.path.dirname(PKG_DIR), "include", "flrl.h")
+
+FRAME_LENGTH = 128
+
+E_OK, E_ARG, E_HIP, E_NOMEM, E_FORMAT, E_TIMEOUT, E_NODEV, E_RCCL = range(8)
+ERROR_NAMES = {
+    E_ARG: "FLRL_E_ARG", E_HIP: "FLRL_E_HIP", E_NOMEM: "FLRL_E_NOMEM",
+    E_FORMAT: "FLRL_E_FORMAT", E_TIMEOUT: "FLRL_E_TIMEOUT", E_NODEV: "FLRL_E_NODEV",
+    E_RCCL: "FLRL_E_RCCL",
+}
+
+GEN_KINDS = {"u8": 0, "lo4": 1, "zero": 2, "runs32": 3, "longruns": 4}
+
+
+class FLRLError(RuntimeError):
+    def __init__(self, code: int, message: str):
+        super().__init__(f"{ERROR_NAMES.get(code, code)}: {message}")
+        self.code = code
+
+
+if not os.path.exists(LIB_PATH):
+    raise ImportError(
+        f"libflrl.so not found at {LIB_PATH}; build it with "
+        f"`make -C {PKG_DIR}` (or __graft_entry__.build())")
+
+_lib = ctypes.CDLL(LIB_PATH)
+
+_u8p = ctypes.POINTER(ctypes.c_uint8)
+_vp = ctypes.c_void_p
+_sz = ctypes.c_size_t
+_u64 = ctypes.c_uint64
+
+
+class _FLBuf(ctypes.Structure):
+    _fields_ = [("bits", _u8p), ("bits_size", _sz), ("values", _u8p),
+                ("values_size", _sz), ("input_size", _sz)]
+
+
+class _RLBuf(ctypes.Structure):
+    _fields_ = [("counts", _u8p), ("values", _u8p), ("runs", _sz), ("input_size", _sz)]
+
+
+def _sig(name, restype, *argtypes):
+    f = getattr(_lib, name)
+    f.restype = restype
+    f.argtypes = list(argtypes)
+    return f
+
+
+_sig("flrl_last_error", ctypes.c_char_p)
+_sig("flrl_version", ctypes.c_char_p)
+_sig("flrl_device_count", ctypes.c_int)
+_sig("flrl_fl_compress", ctypes.c_int, _vp, _sz, ctypes.POINTER(_FLBuf))
+_sig("flrl_fl_compress_sharded", ctypes.c_int, _vp, _sz, ctypes.c_int, ctypes.POINTER(_FLBuf))
+_sig("flrl_fl_decompress", ctypes.c_int, _sz, _vp, _sz, _vp, _sz,
+     ctypes.POINTER(_u8p), ctypes.POINTER(_sz))
+_sig("flrl_fl_scratch_bytes", _sz, _sz)
+_sig("flrl_fl_values_capacity", _sz, _sz)
+_sig("flrl_fl_encode_device", ctypes.c_int, _vp, _sz, _vp, _vp, _vp, _vp, _sz, _vp)
+_sig("flrl_fl_decode_device", ctypes.c_int, _vp, _sz, _vp, _sz, _vp, _sz, _vp, _sz, _vp)
+_sig("flrl_scratch_error", ctypes.c_int, _vp, _vp)
+_sig("flrl_rl_compress", ctypes.c_int, _vp, _sz, ctypes.POINTER(_RLBuf))
+_sig("flrl_rl_decompress", ctypes.c_int, _sz, _vp, _vp, _sz,
+     ctypes.POINTER(_u8p), ctypes.POINTER(_sz))
+_sig("flrl_rl_scratch_bytes", _sz, _sz)
+_sig("flrl_rl_encode_device", ctypes.c_int, _vp, _sz, _vp, _vp, _vp, _vp, _sz, _vp)
+_sig("flrl_rl_decode_scratch_bytes", _sz, _sz)
+_sig("flrl_rl_decode_device", ctypes.c_int, _vp, _vp, _sz, _vp, _sz, _vp, _sz, _vp)
+_sig("flrl_gen_device", ctypes.c_int, ctypes.c_int, _u64, _u64, _vp, _sz, _vp)
+
+_libc = ctypes.CDLL(None)
+_libc.free.argtypes = [_vp]
+_libc.free.restype = None
+
+
+def _check(rc: int):
+    if rc != 0:
+        raise FLRLError(rc, _lib.flrl_last_error().decode(errors="replace"))
+
+
+def _as_u8(data) -> np.ndarray:
+    if isinstance(data, (bytes, bytearray, memoryview)):
+        return np.frombuffer(data, dtype=np.uint8)
+    if isinstance(data, (list, tuple)):
+        return np.asarray(data, dtype=np.uint8)
+    a = np.ascontiguousarray(data)
+    if a.dtype != np.uint8:
+        a = a.view(np.uint8).reshape(-1)
+    return a.reshape(-1)
+
+
+def _take(ptr, n: int) -> np.ndarray:
+    """Copy n bytes out of a malloc'd buffer and free it."""
+    if not ptr:
+        return np.zeros(0, dtype=np.uint8)
+    addr = ctypes.cast(ptr, _vp).value
+    out = np.empty(n, dtype=np.uint8)
+    if n:
+        ctypes.memmove(out.ctypes.data, addr, n)
+    _libc.free(addr)
+    return out
+
+
+@dataclass
+class FLCompressed:
+    """Mirrors FixedLength::FLCompressed (src/fl/fl_common.cuh:11-34)."""
+    bits: np.ndarray
+    values: np.ndarray
+    input_size: int
+
+    def to_file_bytes(self) -> bytes:
+        return fl_file_bytes(self.input_size, self.bits, self.values)
+
+
+@dataclass
+class RLCompressed:
+    counts: np.ndarray
+    values: np.ndarray
+    input_size: int
+
+    def to_file_bytes(self) -> bytes:
+        return rl_file_bytes(self.input_size, self.counts, self.values)
+
+
+def version() -> str:
+    return _lib.flrl_version().decode()
+
+
+def device_count() -> int:
+    return int(_lib.flrl_device_count())
+
+
+# ---------------------------------------------------------------- host API
+def fl_compress(data) -> FLCompressed:
+    a = _as_u8(data)
+    buf = _FLBuf()
+    _check(_lib.flrl_fl_compress(a.ctypes.data if a.size else None, a.size, ctypes.byref(buf)))
+    return FLCompressed(_take(buf.bits, buf.bits_size), _take(buf.values, buf.values_size),
+                        int(buf.input_size))
+
+
+def fl_compress_sharded(data, ngpus: int = 0) -> FLCompressed:
+    a = _as_u8(data)
+    buf = _FLBuf()
+    _check(_lib.flrl_fl_compress_sharded(a.ctypes.data if a.size else None, a.size, ngpus,
+                                         ctypes.byref(buf)))
+    return FLCompressed(_take(buf.bits, buf.bits_size), _take(buf.values, buf.values_size),
+                        int(buf.input_size))
+
+
+def fl_decompress(input_size: int, bits, values) -> np.ndarray:
+    b, v = _as_u8(bits), _as_u8(values)
+    out, out_size = _u8p(), _sz()
+    _check(_lib.flrl_fl_decompress(input_size, b.ctypes.data if b.size else None, b.size,
+                                   v.ctypes.data if v.size else None, v.size,
+                                   ctypes.byref(out), ctypes.byref(out_size)))
+    return _take(out, out_size.value)
+
+
+def rl_compress(data) -> RLCompressed:
+    a = _as_u8(data)
+    buf = _RLBuf()
+    _check(_lib.flrl_rl_compress(a.ctypes.data if a.size else None, a.size, ctypes.byref(buf)))
+    return RLCompressed(_take(buf.counts, buf.runs), _take(buf.values, buf.runs),
+                        int(buf.input_size))
+
+
+def rl_decompress(input_size: int, counts, values) -> np.ndarray:
+    c, v = _as_u8(counts), _as_u8(values)
+    out, out_size = _u8p(), _sz()
+    _check(_lib.flrl_rl_decompress(input_size, c.ctypes.data if c.size else None,
+                                   v.ctypes.data if v.size else None, c.size,
+                                   ctypes.byref(out), ctypes.byref(out_size)))
+    return _take(out, out_size.value)
+
+
+# -------------------------------------------------------------- device API
+def fl_scratch_bytes(n: int) -> int:
+    return int(_lib.flrl_fl_scratch_bytes(n))
+
+
+def fl_values_capacity(n: int) -> int:
+    return int(_lib.flrl_fl_values_capacity(n))
+
+
+def rl_scratch_bytes(n: int) -> int:
+    return int(_lib.flrl_rl_scratch_bytes(n))
+
+
+def rl_decode_scratch_bytes(runs: int) -> int:
+    return int(_lib.flrl_rl_decode_scratch_bytes(runs))
+
+
+def fl_encode_device(d_in: int, n: int, d_bits: int, d_values: int, d_values_size: int,
+                     d_scratch: int, scratch_bytes: int, stream: int = 0) -> None:
+    _check(_lib.flrl_fl_encode_device(d_in, n, d_bits, d_values, d_values_size, d_scratch,
+                                      scratch_bytes, stream or None))
+
+
+def fl_decode_device(d_bits: int, bits_size: int, d_values: int, values_size: int, d_out: int,
+                     n: int, d_scratch: int, scratch_bytes: int, stream: int = 0) -> None:
+    _check(_lib.flrl_fl_decode_device(d_bits, bits_size, d_values, values_size, d_out, n,
+                                      d_scratch, scratch_bytes, stream or None))
+
+
+def rl_encode_device(d_in: int, n: int, d_counts: int, d_values: int, d_runs: int,
+                     d_scratch: int, scratch_bytes: int, stream: int = 0) -> None:
+    _check(_lib.flrl_rl_encode_device(d_in, n, d_counts, d_values, d_runs, d_scratch,
+                                      scratch_bytes, stream or None))
+
+
+def rl_decode_device(d_counts: int, d_values: int, runs: int, d_out: int, n: int,
+                     d_scratch: int, scratch_bytes: int, stream: int = 0) -> None:
+    _check(_lib.flrl_rl_decode_device(d_counts, d_values, runs, d_out, n, d_scratch,
+                                      scratch_bytes, stream or None))
+
+
+def gen_device(kind, seed: int, word_offset: int, d_out: int, n: int, stream: int = 0) -> None:
+    k = GEN_KINDS[kind] if isinstance(kind, str) else int(kind)
+    _check(_lib.flrl_gen_device(k, seed, word_offset, d_out, n, stream or None))
+
+
+def scratch_error(d_scratch: int, stream: int = 0) -> int:
+    rc = _lib.flrl_scratch_error(d_scratch, stream or None)
+    return int(rc)
+
+
+# ------------------------------------------------------------ file formats
+def fl_file_bytes(input_size: int, bits, values) -> bytes:
+    """FL container, byte-identical to the reference (src/file_io.cu:222-280)."""
+    b, v = _as_u8(bits), _as_u8(values)
+    return struct.pack("<QQQ", input_size, b.size, v.size) + b.tobytes() + v.tobytes()
+
+
+def parse_fl_file(blob: bytes) -> FLCompressed:
+    n, fb, vb = struct.unpack_from("<QQQ", blob, 0)
+    if 24 + fb + vb != len(blob):
+        raise ValueError("FL file sizes do not match the header")
+    a = np.frombuffer(blob, dtype=np.uint8)
+    return FLCompressed(a[24:24 + fb].copy(), a[24 + fb:24 + fb + vb].copy(), n)
+
+
+def rl_file_bytes(input_size: int, counts, values) -> bytes:
+    """RL container (build-defined): u64 inputSize | u64 runs | counts | values."""
+    c, v = _as_u8(counts), _as_u8(values)
+    assert c.size == v.size
+    return struct.pack("<QQ", input_size, c.size) + c.tobytes() + v.tobytes()
+
+
+def parse_rl_file(blob: bytes) -> RLCompressed:
+    n, r = struct.unpack_from("<QQ", blob, 0)
+    if 16 + 2 * r != len(blob):
+        raise ValueError("RL file size does not match the header")
+    a = np.frombuffer(blob, dtype=np.uint8)
+    return RLCompressed(a[16:16 + r].copy(), a[16 + r:16 + 2 * r].copy(), n)
+
+
+def declared_symbols(header: str = HEADER_PATH) -> list[str]:
+    """Every function the C ABI header declares."""
+    import re
+    txt = open(header).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(flrl_[a-z0-9_]+)\s*\(", txt)))
+
+
+def lib_handle() -> ctypes.CDLL:
+    return _lib

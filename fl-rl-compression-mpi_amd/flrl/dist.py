@@ -1,0 +1,45 @@
+"""Sharding and the one exchange step of the multi-GPU FL path.
+
+One process per GPU (torch.distributed; backend "nccl" is RCCL over xGMI on
+ROCm, "gloo" for CPU tests). The input byte range is cut into 128-byte-aligned
+shards by the reference rule (src/file_io.cu:46-51: every shard but the last is
+floor(N/(128P))*128 bytes; size_t arithmetic here instead of the reference's
+int). Each rank encodes its shard independently; the only collective is an
+all-gather of {F_r, V_r} (16 bytes per rank) followed by an exclusive scan,
+which places each shard's bits/values in the global output. Concatenating the
+shard outputs in rank order is byte-identical to encoding the whole input
+ — the reference's padded O(P*N) ncclAllGather of the
+payloads (src/fl/fl_gpu.cu:144-238) is not needed.
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+FRAME = 128
+
+
+def shard_range(n: int, rank: int, world: int) -> tuple[int, int]:
+    """(start, length) of rank's shard of an n-byte input (file_io.cu:46-51)."""
+    per = (n // (FRAME * world)) * FRAME
+    start = rank * per
+    length = n - (world - 1) * per if rank == world - 1 else per
+    return start, length
+
+
+def size_scan(sizes: torch.Tensor, group=None) -> tuple[torch.Tensor, torch.Tensor]:
+    """All-gather each rank's int64 [F_r, V_r] and exclusive-scan them.
+
+    `sizes` stays on its device (no host sync for a GPU tensor). Returns
+    (offsets of this rank [F_off, V_off], totals [F, V]) as int64 tensors on
+    the same device.
+    """
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    sizes = sizes.reshape(2).to(torch.int64)
+    parts = [torch.empty_like(sizes) for _ in range(world)]
+    dist.all_gather(parts, sizes, group=group)
+    allsz = torch.stack(parts)               # [world, 2]
+    incl = torch.cumsum(allsz, dim=0)
+    excl = incl - allsz
+    return excl[rank], incl[-1]

@@ -1,0 +1,178 @@
+// main.cpp — the `compress` CLI (reference: src/main.cu:18-169).
+//
+//   compress c <method> <input> <output>     compress a file
+//   compress d <method> <input> <output>     decompress a file
+//
+// fl / fl-mpi / fl-nccl / fl-shmem / rl run on the GPU through the C ABI in
+// include/flrl.h (libflrl.so); fl-cpu / rl-cpu run the host codec. Errors print
+// "[ERROR]: <message>" to stderr like the reference (main.cu:95-98), but the
+// process then exits with status 2 instead of 0, and no partial output file is
+// left behind. Phase timings print as the reference's "[TIMER]" lines.
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <stdexcept>
+#include <string>
+#include <thread>
+
+#include "args_parser.hpp"
+#include "cpu_codec.hpp"
+#include "file_io.hpp"
+#include "flrl.h"
+
+using namespace flrl_cli;
+
+namespace {
+
+struct Timer {
+    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+    void done(const char *step)
+    {
+        const double ms = std::chrono::duration<double, std::milli>(
+                              std::chrono::steady_clock::now() - t0)
+                              .count();
+        std::printf("[TIMER] Step: \"%s\", Time: %.3f ms\n", step, ms);
+        t0 = std::chrono::steady_clock::now();
+    }
+};
+
+void check(int rc, const char *what)
+{
+    if (rc != FLRL_OK)
+        throw std::runtime_error(std::string(what) + ": " + flrl_last_error());
+}
+
+unsigned host_threads()
+{
+    const unsigned h = std::thread::hardware_concurrency();
+    return h ? h : 1;
+}
+
+bool is_gpu(Method m)
+{
+    return m == Method::FixedLength || m == Method::FixedLengthMulti || m == Method::RunLength;
+}
+
+void compress(const Args &a)
+{
+    Timer t;
+    FileData in = loadFile(a.inputFile);
+    t.done("Load data from file");
+    const bool rl = a.method == Method::RunLength || a.method == Method::RunLengthCPU;
+    try {
+        if (!rl) {
+            flrl_fl_buf c{};
+            switch (a.method) {
+            case Method::FixedLength:
+                check(flrl_fl_compress(in.data, in.size, &c), "fl compress");
+                break;
+            case Method::FixedLengthMulti:
+                check(flrl_fl_compress_sharded(in.data, in.size, 0, &c), "fl sharded compress");
+                break;
+            default:
+                c = cpuCompressFL(in.data, in.size, host_threads());
+                break;
+            }
+            t.done("Compression");
+            try {
+                saveCompressedFL(a.outputFile, c);
+            } catch (...) {
+                std::free(c.bits);
+                std::free(c.values);
+                throw;
+            }
+            std::free(c.bits);
+            std::free(c.values);
+        } else {
+            flrl_rl_buf c{};
+            if (a.method == Method::RunLength)
+                check(flrl_rl_compress(in.data, in.size, &c), "rl compress");
+            else
+                c = cpuCompressRL(in.data, in.size);
+            t.done("Compression");
+            try {
+                saveCompressedRL(a.outputFile, c);
+            } catch (...) {
+                std::free(c.counts);
+                std::free(c.values);
+                throw;
+            }
+            std::free(c.counts);
+            std::free(c.values);
+        }
+        t.done("Save data to file");
+    } catch (...) {
+        std::free(in.data);
+        throw;
+    }
+    std::free(in.data);
+}
+
+void decompress(const Args &a)
+{
+    Timer t;
+    FileData out;
+    const bool rl = a.method == Method::RunLength || a.method == Method::RunLengthCPU;
+    if (!rl) {
+        flrl_fl_buf c = loadCompressedFL(a.inputFile);
+        t.done("Load data from file");
+        try {
+            if (is_gpu(a.method))
+                check(flrl_fl_decompress(c.input_size, c.bits, c.bits_size, c.values,
+                                         c.values_size, &out.data, &out.size),
+                      "fl decompress");
+            else
+                cpuDecompressFL(c, &out.data, &out.size, host_threads());
+        } catch (...) {
+            std::free(c.bits);
+            std::free(c.values);
+            throw;
+        }
+        std::free(c.bits);
+        std::free(c.values);
+    } else {
+        flrl_rl_buf c = loadCompressedRL(a.inputFile);
+        t.done("Load data from file");
+        try {
+            if (is_gpu(a.method))
+                check(flrl_rl_decompress(c.input_size, c.counts, c.values, c.runs, &out.data,
+                                         &out.size),
+                      "rl decompress");
+            else
+                cpuDecompressRL(c, &out.data, &out.size);
+        } catch (...) {
+            std::free(c.counts);
+            std::free(c.values);
+            throw;
+        }
+        std::free(c.counts);
+        std::free(c.values);
+    }
+    t.done("Decompression");
+    try {
+        saveFile(a.outputFile, out);
+    } catch (...) {
+        std::free(out.data);
+        throw;
+    }
+    std::free(out.data);
+    t.done("Save data to file");
+}
+
+}  // namespace
+
+int main(int argc, char **argv)
+{
+    const Args a = parseArguments(argc, argv);
+    try {
+        if (a.operation == Operation::Compression)
+            compress(a);
+        else
+            decompress(a);
+    } catch (const std::exception &e) {
+        std::fprintf(stderr, "[ERROR]: %s\n", e.what());
+        std::remove(a.outputFile);
+        return 2;
+    }
+    return 0;
+}

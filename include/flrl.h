@@ -1,0 +1,147 @@
+/*
+ * flrl.h — C ABI of the MI355X-native fixed-length (FL) / run-length (RL) codec.
+ *
+ * Drop-in boundary for the reference's codec functions (namespace FixedLength in
+ * Polyphemus980/fl-rl-compression-MPI). Every entry point is plain C: pointers,
+ * sizes, int status codes; no HIP or torch types. Streams are passed as `void*`
+ * (a hipStream_t; NULL = the default stream).
+ *
+ * Status codes: 0 = ok, nonzero = error (see FLRL_E_*); flrl_last_error()
+ * returns the message of the calling thread's last failure. Host-buffer
+ * functions are synchronous and return malloc'd buffers the caller releases
+ * with free() (the reference's ownership rule: fl_cpu.cu:23,54,104 malloc,
+ * main.cu:126-128,155-156,168 free). Device functions are asynchronous on the
+ * given stream; their data-dependent errors (bad widths, size mismatch) land in
+ * the scratch area and are read with flrl_scratch_error().
+ *
+ * File formats:
+ *  FL (byte-identical to the reference, file_io.cu:222-280 / :117-192):
+ *     u64 inputSize | u64 bitsSize | u64 valuesSize | u8 bits[bitsSize] | u8 values[valuesSize]
+ *  RL (build-defined; the reference has no RL code):
+ *     u64 inputSize | u64 runs | u8 counts[runs] | u8 values[runs]
+ */
+#ifndef FLRL_H
+#define FLRL_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FLRL_FRAME_LENGTH 128 /* FRAME_LENGTH, src/fl/fl_common.cuh:9 */
+
+enum {
+    FLRL_OK = 0,
+    FLRL_E_ARG = 1,        /* bad argument (null pointer, capacity too small) */
+    FLRL_E_HIP = 2,        /* HIP runtime error (message in flrl_last_error) */
+    FLRL_E_NOMEM = 3,      /* host/device allocation failed ("Cannot allocate memory") */
+    FLRL_E_FORMAT = 4,     /* malformed compressed data (width not in [1,8], size mismatch) */
+    FLRL_E_TIMEOUT = 5,    /* in-kernel look-back did not complete (should never happen) */
+    FLRL_E_NODEV = 6,      /* no HIP device */
+    FLRL_E_RCCL = 7        /* RCCL error in the sharded path */
+};
+
+/* Mirrors FixedLength::FLCompressed, src/fl/fl_common.cuh:11-34. */
+typedef struct flrl_fl_buf {
+    uint8_t *bits;        /* per-frame bit width b in [1,8], bits_size = ceil(n/128) */
+    size_t bits_size;
+    uint8_t *values;      /* LSB-first packed values, values_size bytes */
+    size_t values_size;
+    size_t input_size;
+} flrl_fl_buf;
+
+/* RL analogue (build-defined). */
+typedef struct flrl_rl_buf {
+    uint8_t *counts;      /* run lengths, each in [1,255] */
+    uint8_t *values;      /* run byte values */
+    size_t runs;
+    size_t input_size;
+} flrl_rl_buf;
+
+/* ---- library / errors ---------------------------------------------------- */
+const char *flrl_last_error(void);       /* thread-local; "" when none */
+const char *flrl_version(void);
+int flrl_device_count(void);             /* number of visible HIP devices (0 if none) */
+
+/* ---- FL, host buffers (synchronous) ---------------------------------------
+ * flrl_fl_compress replaces FixedLength::gpuCompress (src/fl/fl_gpu.cuh:14,
+ * fl_gpu.cu:289-423) and its CPU twin cpuCompress (src/fl/fl_cpu.cuh:9). On
+ * size == 0 it returns an all-zero flrl_fl_buf (fl_gpu.cu:291-294). */
+int flrl_fl_compress(const uint8_t *data, size_t size, flrl_fl_buf *out);
+
+/* Replaces FixedLength::gpuDecompress (src/fl/fl_gpu.cuh:15, fl_gpu.cu:537-645)
+ * and cpuDecompress (src/fl/fl_cpu.cuh:10). Keeps the reference's early-out: if
+ * values_size == 0 || bits_size == 0 the result is empty (*out = NULL,
+ * *out_size = 0; fl_cpu.cu:94-97). Unlike the reference it validates the
+ * frame widths (each in [1,8]), bits_size == ceil(output_size/128) and
+ * values_size == the size the widths imply, returning FLRL_E_FORMAT otherwise. */
+int flrl_fl_decompress(size_t output_size, const uint8_t *bits, size_t bits_size,
+                       const uint8_t *values, size_t values_size,
+                       uint8_t **out, size_t *out_size);
+
+/* Sharded encode across `ngpus` GPUs of this node (<= 0: all visible), one
+ * process. Replaces FixedLength::gpuNCCLCompress (src/fl/fl_gpu.cuh:16,
+ * fl_gpu.cu:76-287) and gpuMPICompress (fl_gpu.cuh:13, fl_gpu.cu:41-74):
+ * 128-aligned shards by the reference rule (file_io.cu:46-51, size_t here),
+ * one RCCL AllGather of {F_r, V_r} + exclusive scan to place the outputs. The
+ * result is byte-identical to flrl_fl_compress. */
+int flrl_fl_compress_sharded(const uint8_t *data, size_t size, int ngpus, flrl_fl_buf *out);
+
+/* ---- FL, device-resident (asynchronous on `stream`) -----------------------
+ * Replaces FixedLength::gpuCompressDevice (src/fl/fl_gpu.cuh:17,
+ * fl_gpu.cu:425-535) — outputs stay in HBM.
+ * All device pointers must be 16-byte aligned (hipMalloc / torch allocations
+ * are); FLRL_E_ARG otherwise.
+ *   d_in        n input bytes
+ *   d_bits      ceil(n/128) bytes
+ *   d_values    capacity >= flrl_fl_values_capacity(n) bytes
+ *   d_values_size  device u64 receiving valuesSize
+ *   d_scratch   >= flrl_fl_scratch_bytes(n) bytes of device memory, 16-B aligned
+ * n == 0 writes 0 to *d_values_size. */
+size_t flrl_fl_scratch_bytes(size_t n);
+size_t flrl_fl_values_capacity(size_t n);
+int flrl_fl_encode_device(const uint8_t *d_in, size_t n, uint8_t *d_bits, uint8_t *d_values,
+                          uint64_t *d_values_size, void *d_scratch, size_t scratch_bytes,
+                          void *stream);
+
+/* Device decode: n output bytes from bits/values. The kernel flags
+ * FLRL_E_FORMAT in the scratch area when a width is outside [1,8] or
+ * values_size differs from the size the widths imply. */
+int flrl_fl_decode_device(const uint8_t *d_bits, size_t bits_size, const uint8_t *d_values,
+                          size_t values_size, uint8_t *d_out, size_t n, void *d_scratch,
+                          size_t scratch_bytes, void *stream);
+
+/* Reads (synchronising `stream`) the error word a device call left in scratch:
+ * 0 = ok, else an FLRL_E_* code. */
+int flrl_scratch_error(const void *d_scratch, void *stream);
+
+/* ---- RL, host buffers (synchronous) --------------------------------------- */
+int flrl_rl_compress(const uint8_t *data, size_t size, flrl_rl_buf *out);
+int flrl_rl_decompress(size_t output_size, const uint8_t *counts, const uint8_t *values,
+                       size_t runs, uint8_t **out, size_t *out_size);
+
+/* ---- RL, device-resident (asynchronous) ----------------------------------
+ * d_counts / d_values capacity n bytes each; d_runs receives R (device u64). */
+size_t flrl_rl_scratch_bytes(size_t n);
+int flrl_rl_encode_device(const uint8_t *d_in, size_t n, uint8_t *d_counts, uint8_t *d_values,
+                          uint64_t *d_runs, void *d_scratch, size_t scratch_bytes, void *stream);
+/* Decode R runs into n = sum(counts) bytes; flags FLRL_E_FORMAT in scratch if a
+ * count is 0 or the counts do not sum to n. */
+size_t flrl_rl_decode_scratch_bytes(size_t runs);
+int flrl_rl_decode_device(const uint8_t *d_counts, const uint8_t *d_values, size_t runs,
+                          uint8_t *d_out, size_t n, void *d_scratch, size_t scratch_bytes,
+                          void *stream);
+
+/* ---- synthetic inputs on device (SURVEY.md §8(d) generator) ---------------
+ * kind 0 u8, 1 lo4, 2 zero (counter-based; word_offset = global 8-byte word index
+ * of d_out[0], so a shard at byte offset 8*k reproduces the whole buffer's bytes). */
+int flrl_gen_device(int kind, uint64_t seed, uint64_t word_offset, uint8_t *d_out, size_t n,
+                    void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* FLRL_H */

@@ -1,0 +1,65 @@
+"""The C-ABI library loads and exports every symbol include/flrl.h declares
+(no compute calls: runs without a GPU)."""
+import ctypes
+import os
+import subprocess
+
+import pytest
+
+import flrl
+
+
+def test_exports_every_declared_symbol():
+    syms = flrl.declared_symbols()
+    assert len(syms) >= 18
+    lib = flrl.lib_handle()
+    missing = [s for s in syms if not hasattr(lib, s)]
+    assert not missing, f"declared but not exported: {missing}"
+
+
+def test_exports_are_c_linkage():
+    out = subprocess.run(["nm", "-D", "--defined-only", flrl.LIB_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    exported = {line.split()[-1] for line in out.splitlines() if " T " in line}
+    for s in flrl.declared_symbols():
+        assert s in exported, s
+
+
+def test_gfx950_code_object():
+    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", flrl.LIB_PATH],
+                         capture_output=True, text=True)
+    text = out.stdout + out.stderr
+    if "gfx950" not in text:  # older objdump: fall back to the bundle string
+        with open(flrl.LIB_PATH, "rb") as f:
+            assert b"gfx950" in f.read()
+
+
+def test_sizing_functions_are_pure():
+    assert flrl.fl_values_capacity(0) == 16
+    assert flrl.fl_values_capacity(17) == 32
+    s1 = flrl.fl_scratch_bytes(1)
+    s2 = flrl.fl_scratch_bytes(1 << 30)
+    assert s1 >= 24 and s2 > s1 and s2 % 16 == 0
+    assert flrl.version().startswith("flrl")
+
+
+def test_no_silent_cpu_fallback_without_device():
+    if flrl.device_count() > 0:
+        pytest.skip("a HIP device is visible")
+    with pytest.raises(flrl.FLRLError) as e:
+        flrl.fl_compress(b"abc")
+    assert e.value.code == flrl.E_NODEV
+    # empty input never needs the device (fl_gpu.cu:291-294)
+    assert flrl.fl_compress(b"").input_size == 0
+
+
+def test_file_format_helpers():
+    import numpy as np
+    blob = flrl.fl_file_bytes(5, np.array([3], np.uint8), np.array([1, 2], np.uint8))
+    assert blob[:24] == (5).to_bytes(8, "little") + (1).to_bytes(8, "little") + (2).to_bytes(8, "little")
+    c = flrl.parse_fl_file(blob)
+    assert c.input_size == 5 and c.bits.tolist() == [3] and c.values.tolist() == [1, 2]
+    r = flrl.parse_rl_file(flrl.rl_file_bytes(4, [1, 3], [9, 8]))
+    assert r.input_size == 4 and r.counts.tolist() == [1, 3] and r.values.tolist() == [9, 8]
+    with pytest.raises(ValueError):
+        flrl.parse_fl_file(blob[:-1])

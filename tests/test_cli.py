@@ -1,0 +1,107 @@
+"""The `compress` CLI (reference src/main.cu, src/args_parser.cu) on host-only
+methods: fl-cpu output is byte-identical to the reference's fl-cpu (golden
+sha256), rl-cpu round-trips and matches the oracle, usage errors exit 1,
+malformed files are rejected."""
+import hashlib
+import subprocess
+
+import numpy as np
+import pytest
+
+import flrl
+import oracle
+
+
+def run(cli, *args, check=True):
+    return subprocess.run([cli, *map(str, args)], capture_output=True, text=True, check=check)
+
+
+def sha(b) -> str:
+    return hashlib.sha256(bytes(b)).hexdigest()
+
+
+def test_fl_cpu_bmp_matches_reference(cli_path, golden, bmp_bytes, tmp_path):
+    src = tmp_path / "in.bmp"
+    src.write_bytes(bmp_bytes)
+    r = run(cli_path, "c", "fl-cpu", src, tmp_path / "o.fl")
+    assert '[TIMER] Step: "Compression"' in r.stdout
+    assert sha((tmp_path / "o.fl").read_bytes()) == golden["fl_bmp"]["fl_sha256"]
+    run(cli_path, "d", "fl-cpu", tmp_path / "o.fl", tmp_path / "back.bin")
+    assert (tmp_path / "back.bin").read_bytes() == bmp_bytes
+
+
+@pytest.mark.parametrize("idx", range(7))
+def test_fl_cpu_generated(cli_path, golden, tmp_path, idx):
+    g = golden["fl_generated"][idx]
+    a = oracle.gen(g["kind"], g["n"], g["seed"])
+    (tmp_path / "in").write_bytes(a.tobytes())
+    run(cli_path, "c", "fl-cpu", tmp_path / "in", tmp_path / "o.fl")
+    assert sha((tmp_path / "o.fl").read_bytes()) == g["fl_sha256"]
+
+
+def test_fl_cpu_empty(cli_path, golden, tmp_path):
+    (tmp_path / "e").write_bytes(b"")
+    run(cli_path, "c", "fl-cpu", tmp_path / "e", tmp_path / "e.fl")
+    assert sha((tmp_path / "e.fl").read_bytes()) == golden["fl_empty_file_sha256"]
+    run(cli_path, "d", "fl-cpu", tmp_path / "e.fl", tmp_path / "e.out")
+    assert (tmp_path / "e.out").read_bytes() == b""
+
+
+@pytest.mark.parametrize("kind", ["runs32", "longruns", "u8", "zero"])
+def test_rl_cpu_roundtrip_matches_oracle(cli_path, tmp_path, kind):
+    a = oracle.gen(kind, 200_003, 8)
+    (tmp_path / "in").write_bytes(a.tobytes())
+    run(cli_path, "c", "rl-cpu", tmp_path / "in", tmp_path / "o.rl")
+    blob = (tmp_path / "o.rl").read_bytes()
+    counts, values = oracle.rl_compress(a)
+    assert blob == flrl.rl_file_bytes(a.size, counts, values)
+    run(cli_path, "d", "rl-cpu", tmp_path / "o.rl", tmp_path / "back")
+    assert (tmp_path / "back").read_bytes() == a.tobytes()
+
+
+def test_rl_cpu_kats(cli_path, golden, tmp_path):
+    from conftest import kat_input
+    for case in golden["rl_kat"]:
+        data = kat_input(case)
+        (tmp_path / "in").write_bytes(data)
+        run(cli_path, "c", "rl-cpu", tmp_path / "in", tmp_path / "o.rl")
+        r = flrl.parse_rl_file((tmp_path / "o.rl").read_bytes())
+        assert r.counts.tolist() == case["counts"] and r.values.tolist() == case["values"]
+
+
+@pytest.mark.parametrize("argv", [[], ["c"], ["x", "fl", "a", "b"], ["c", "zz", "a", "b"],
+                                  ["c", "fl", "a", "b", "extra"]])
+def test_usage_errors_exit_1(cli_path, argv):
+    r = run(cli_path, *argv, check=False)
+    assert r.returncode == 1
+    assert "USAGE" in r.stderr
+
+
+def test_missing_input_reports_error(cli_path, tmp_path):
+    r = run(cli_path, "c", "fl-cpu", tmp_path / "nope", tmp_path / "o", check=False)
+    assert r.returncode == 2 and "[ERROR]:" in r.stderr
+    assert not (tmp_path / "o").exists()
+
+
+def test_malformed_fl_files_rejected(cli_path, tmp_path):
+    a = oracle.gen("lo4", 3000, 1)
+    good = oracle.fl_file_bytes(a)
+    cases = {
+        "truncated_header": good[:20],
+        "truncated_values": good[:-3],
+        "bad_width": good[:24] + bytes([0]) + good[25:],
+        "width9": good[:24] + bytes([9]) + good[25:],
+        "bits_size_lies": (3000).to_bytes(8, "little") + (5).to_bytes(8, "little") + good[16:],
+    }
+    for name, blob in cases.items():
+        (tmp_path / name).write_bytes(blob)
+        r = run(cli_path, "d", "fl-cpu", tmp_path / name, tmp_path / "out", check=False)
+        assert r.returncode == 2, name
+        assert "[ERROR]:" in r.stderr, name
+
+
+def test_malformed_rl_files_rejected(cli_path, tmp_path):
+    blob = flrl.rl_file_bytes(5, [2, 0], [1, 1])  # zero count / wrong sum
+    (tmp_path / "bad.rl").write_bytes(blob)
+    r = run(cli_path, "d", "rl-cpu", tmp_path / "bad.rl", tmp_path / "o", check=False)
+    assert r.returncode == 2

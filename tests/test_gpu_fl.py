@@ -1,0 +1,255 @@
+"""FL parity on the MI355X: HIP path (through the C ABI) vs the CPU oracle.
+
+Bit-exact on every case: golden vectors of the reference fl-cpu, seeded
+inputs at oracle-checkable sizes (edges of frames, 16-byte lanes and 64 KiB
+tiles; every width 1..8 inside one tile), and at full BASELINE sizes the
+size-independent properties: golden sha256 of the 1 GiB configs, decode(encode)
+round trips, and shard-equivalence against the oracle on sampled 128-aligned
+windows of a 16 GiB input.
+"""
+import hashlib
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import flrl
+import oracle
+from conftest import kat_input
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available() or flrl.device_count() == 0:
+        pytest.fail("GPU tests need a HIP device")  # never silently skip on the GPU box
+
+
+def sha(b) -> str:
+    return hashlib.sha256(bytes(b)).hexdigest()
+
+
+def mixed_width_input(n: int, seed: int) -> np.ndarray:
+    """Every frame gets a random width in [1,8] (and some frames all-zero)."""
+    rng = np.random.default_rng(seed)
+    frames = (n + 127) // 128
+    widths = rng.integers(0, 9, size=frames)
+    hi = np.repeat((1 << widths) - 1, 128)[:n]
+    a = (rng.integers(0, 256, size=n) & hi).astype(np.uint8)
+    return a
+
+
+def check_against_oracle(a: np.ndarray):
+    c = flrl.fl_compress(a)
+    bits, values = oracle.fl_compress(a)
+    assert c.input_size == a.size
+    assert np.array_equal(c.bits, bits)
+    assert np.array_equal(c.values, values)
+    back = flrl.fl_decompress(a.size, c.bits, c.values)
+    assert np.array_equal(back, a)
+    return c
+
+
+def test_kats(golden):
+    for case in golden["fl_kat"]:
+        data = kat_input(case)
+        c = flrl.fl_compress(data)
+        assert c.bits.tobytes().hex() == case["bits_hex"], case["name"]
+        assert c.values.tobytes().hex() == case["values_hex"], case["name"]
+        assert flrl.fl_decompress(len(data), c.bits, c.values).tobytes() == data
+
+
+def test_empty(golden):
+    c = flrl.fl_compress(b"")
+    assert c.bits.size == 0 and c.values.size == 0 and c.input_size == 0
+    assert sha(c.to_file_bytes()) == golden["fl_empty_file_sha256"]
+    assert flrl.fl_decompress(0, c.bits, c.values).size == 0
+
+
+def test_bmp(golden, bmp_bytes):
+    c = flrl.fl_compress(bmp_bytes)
+    assert sha(c.to_file_bytes()) == golden["fl_bmp"]["fl_sha256"]
+    assert flrl.fl_decompress(c.input_size, c.bits, c.values).tobytes() == bmp_bytes
+
+
+@pytest.mark.parametrize("idx", range(7))
+def test_generated_golden(golden, idx):
+    g = golden["fl_generated"][idx]
+    a = oracle.gen(g["kind"], g["n"], g["seed"])
+    c = flrl.fl_compress(a)
+    assert sha(c.to_file_bytes()) == g["fl_sha256"]
+    assert np.array_equal(flrl.fl_decompress(a.size, c.bits, c.values), a)
+
+
+SIZES = [1, 2, 7, 8, 15, 16, 17, 127, 128, 129, 255, 256, 1000, 4096, 4741, 65535, 65536,
+         65537, 100003, 131072, 131073, 262144 + 4095, (1 << 20) + 13]
+
+
+@pytest.mark.parametrize("n", SIZES)
+@pytest.mark.parametrize("kind", ["u8", "lo4", "zero", "ff", "mixed"])
+def test_sizes_vs_oracle(n, kind):
+    if kind == "ff":
+        a = np.full(n, 255, np.uint8)
+    elif kind == "mixed":
+        a = mixed_width_input(n, n)
+    else:
+        a = oracle.gen(kind, n, 11)
+    check_against_oracle(a)
+
+
+def test_every_width_in_one_tile():
+    # width b in frame f = 1 + f % 8, max value present in each frame
+    frames = 1024
+    a = np.zeros(frames * 128, np.uint8)
+    for f in range(frames):
+        b = 1 + f % 8
+        a[f * 128:(f + 1) * 128] = np.arange(128) % (1 << b)
+        a[f * 128 + 5] = (1 << b) - 1
+    c = check_against_oracle(a)
+    assert c.bits.tolist() == [1 + f % 8 for f in range(frames)]
+
+
+def test_many_tiles_random_widths():
+    a = mixed_width_input(64 * 65536 + 777, 5)  # 65 tiles: look-back over > 64 tiles
+    check_against_oracle(a)
+
+
+# ------------------------------------------------------------- malformed input
+def test_decode_rejects_bad_width():
+    a = oracle.gen("lo4", 1000, 1)
+    c = flrl.fl_compress(a)
+    for bad in (0, 9, 255):
+        bits = c.bits.copy()
+        bits[3] = bad
+        with pytest.raises(flrl.FLRLError) as e:
+            flrl.fl_decompress(a.size, bits, c.values)
+        assert e.value.code == flrl.E_FORMAT
+
+
+def test_decode_rejects_size_mismatch():
+    a = oracle.gen("u8", 5000, 1)
+    c = flrl.fl_compress(a)
+    with pytest.raises(flrl.FLRLError):
+        flrl.fl_decompress(a.size, c.bits, c.values[:-1])
+    with pytest.raises(flrl.FLRLError):
+        flrl.fl_decompress(a.size + 128, c.bits, c.values)
+
+
+def test_decode_reference_early_out():
+    # fl_cpu.cu:94-97: valuesSize == 0 || bitsSize == 0 -> empty output
+    assert flrl.fl_decompress(100, np.zeros(0, np.uint8), np.ones(4, np.uint8)).size == 0
+    assert flrl.fl_decompress(100, np.ones(1, np.uint8), np.zeros(0, np.uint8)).size == 0
+
+
+# ----------------------------------------------------- device API, full sizes
+def test_device_api_errors():
+    from flrl.device import FLDevice
+    d = FLDevice(4096)
+    x = torch.zeros(4096 + 32, dtype=torch.uint8, device="cuda")
+    with pytest.raises(flrl.FLRLError) as e:
+        flrl.fl_encode_device(x.data_ptr() + 1, 4096, d.bits.data_ptr(), d.values.data_ptr(),
+                              d.sizes.data_ptr() + 8, d.scratch.data_ptr(), d.scratch_bytes)
+    assert e.value.code == flrl.E_ARG
+    with pytest.raises(flrl.FLRLError):
+        flrl.fl_encode_device(x.data_ptr(), 4096, d.bits.data_ptr(), d.values.data_ptr(),
+                              d.sizes.data_ptr() + 8, d.scratch.data_ptr(), 8)
+
+
+def test_device_bad_width_flag():
+    from flrl.device import FLDevice
+    n = 300_000
+    a = torch.from_numpy(oracle.gen("lo4", n, 2)).cuda()
+    d = FLDevice(n)
+    d.encode(a)
+    v = d.values_size()
+    assert d.error() == 0
+    d.bits[1234] = 0
+    d.decode(v)
+    assert d.error() == flrl.E_FORMAT
+
+
+@pytest.mark.parametrize("idx", [0, 1])
+def test_device_1gib_golden(golden, idx):
+    """Config #2 (u8) and the lo4 twin at 1 GiB: file sha256 == reference fl-cpu."""
+    from flrl.device import FLDevice, gen
+    g = golden["fl_generated_large"][idx]
+    n = g["n"]
+    x = gen(g["kind"], n, g["seed"])
+    d = FLDevice(n)
+    d.encode(x)
+    v = d.values_size()
+    assert d.error() == 0
+    h = hashlib.sha256()
+    h.update(np.array([n, d.frames, v], dtype="<u8").tobytes())
+    h.update(d.bits[: d.frames].cpu().numpy().tobytes())
+    h.update(d.values[:v].cpu().numpy().tobytes())
+    assert h.hexdigest() == g["fl_sha256"]
+    assert 24 + d.frames + v == g["fl_bytes"]
+    xin = hashlib.sha256(x[:n].cpu().numpy().tobytes()).hexdigest()
+    assert xin == g["input_sha256"]
+    out = d.decode(v)
+    assert d.error() == 0
+    assert torch.equal(out, x[:n])
+
+
+def test_device_16gib_lo4_shard_equivalence():
+    """Config #4: 16 GiB lo4 on one GPU. Round trip on device, and 128-aligned
+    windows of the input re-encoded by the oracle equal the matching slices of
+    the GPU output."""
+    from flrl.device import FLDevice, gen
+    n = 16 << 30
+    x = gen("lo4", n, 42)
+    x[(12 << 30) + 77] = 0xF3  # a wide frame deep in the buffer
+    d = FLDevice(n)
+    d.encode(x)
+    v = d.values_size()
+    assert d.error() == 0
+    bits = d.bits[: d.frames]
+    assert int(bits.min()) >= 1 and int(bits.max()) <= 8
+    pref = torch.cumsum(bits.to(torch.int64), 0) * 16  # byte end of each frame
+    assert int(pref[-1]) == v
+    rng = np.random.default_rng(0)
+    starts = [0, ((12 << 30) + 77) // 128 * 128 - 100 * 128, (d.frames - 4096) * 128] + \
+        [int(s) * 128 for s in rng.integers(0, d.frames - 4096, size=3)]
+    for s in starts:
+        L = 4096 * 128
+        f0 = s // 128
+        ob, ov = oracle.fl_compress(x[s:s + L].cpu().numpy())
+        assert np.array_equal(bits[f0:f0 + 4096].cpu().numpy(), ob)
+        v0 = 0 if f0 == 0 else int(pref[f0 - 1])
+        assert np.array_equal(d.values[v0:v0 + ov.size].cpu().numpy(), ov)
+    out = d.decode(v)
+    assert d.error() == 0
+    assert torch.equal(out, x[:n])
+    del d, x, out
+    torch.cuda.empty_cache()
+
+
+# ------------------------------------------------------------------ sharded
+def test_sharded_equals_single(bmp_bytes):
+    ng = flrl.device_count()
+    c1 = flrl.fl_compress(bmp_bytes)
+    for p in range(1, ng + 1):
+        cp = flrl.fl_compress_sharded(bmp_bytes, p)
+        assert np.array_equal(cp.bits, c1.bits) and np.array_equal(cp.values, c1.values)
+    with pytest.raises(flrl.FLRLError):
+        flrl.fl_compress_sharded(bmp_bytes, ng + 1)
+
+
+# ---------------------------------------------------------------------- CLI
+def test_cli_gpu_methods(golden, bmp_bytes, cli_path, tmp_path):
+    src = tmp_path / "in.bmp"
+    src.write_bytes(bmp_bytes)
+    for method in ("fl", "fl-nccl", "fl-mpi", "fl-shmem"):
+        out = tmp_path / f"o.{method}"
+        subprocess.run([cli_path, "c", method, str(src), str(out)], check=True,
+                       capture_output=True)
+        assert sha(out.read_bytes()) == golden["fl_bmp"]["fl_sha256"], method
+        back = tmp_path / f"b.{method}"
+        subprocess.run([cli_path, "d", method, str(out), str(back)], check=True,
+                       capture_output=True)
+        assert back.read_bytes() == bmp_bytes
