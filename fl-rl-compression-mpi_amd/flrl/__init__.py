@@ -51,6 +51,16 @@ class FLRLError(RuntimeError):
         self.code = code
 
 
+# torch-ROCm bundles its own libamdhip64.so.7 with the same soname as
+# /opt/rocm's; whichever is loaded first serves the whole process. Load torch's
+# first (when torch is installed) so device pointers and streams from torch and
+# from libflrl.so belong to one HIP runtime; loading /opt/rocm's first leaves
+# torch without a usable device.
+try:
+    import torch as _torch  # noqa: F401
+except ImportError:
+    _torch = None
+
 if not os.path.exists(LIB_PATH):
     raise ImportError(
         f"libflrl.so not found at {LIB_PATH}; build it with "

@@ -25,8 +25,12 @@ torch = pytest.importorskip("torch")
 
 @pytest.fixture(scope="module", autouse=True)
 def _need_gpu():
-    if not torch.cuda.is_available() or flrl.device_count() == 0:
-        pytest.fail("GPU tests need a HIP device")  # never silently skip on the GPU box
+    avail, ndev = torch.cuda.is_available(), flrl.device_count()
+    if not avail or ndev == 0:  # never silently skip on the GPU box
+        pytest.fail(f"GPU tests need a HIP device (torch: {avail}, flrl: {ndev}, "
+                    f"HIP_VISIBLE_DEVICES={os.environ.get('HIP_VISIBLE_DEVICES')}, "
+                    f"CUDA_VISIBLE_DEVICES={os.environ.get('CUDA_VISIBLE_DEVICES')}, "
+                    f"ROCR_VISIBLE_DEVICES={os.environ.get('ROCR_VISIBLE_DEVICES')})")
 
 
 def sha(b) -> str:
