@@ -139,6 +139,16 @@ def main():
         codec.decode(v, out=out)
     torch.cuda.synchronize()
 
+    # ---- practical HBM ceiling on these buffers: a plain device copy (read N + write N)
+    cp = [torch.cuda.Event(enable_timing=True) for _ in range(6)]
+    for i in range(3):
+        cp[2 * i].record(stream)
+        out[:n].copy_(x[:n])
+        cp[2 * i + 1].record(stream)
+    torch.cuda.synchronize()
+    copy_ms = min(cp[2 * i].elapsed_time(cp[2 * i + 1]) for i in range(3))
+    copy_gbs = 2 * n / (copy_ms * 1e-3) / 1e9
+
     # ---- timed region: K steps ----
     ev = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(args.steps)]
     if world > 1:
@@ -233,6 +243,8 @@ def main():
                 "fl_decode": {"ms": round(dec_ms, 4), "alg_GBps": round(dec_gbs, 1),
                               "output_GBps": round(n / (dec_ms * 1e-3) / 1e9, 1)},
                 "size_scan": {"ms": round(scan_ms, 4)},
+                "device_copy_ceiling": {"ms": round(copy_ms, 4), "GBps": round(copy_gbs, 1),
+                                        "note": "torch copy_ of the same N bytes (read N + write N)"},
             },
             "cpu_baseline": cpu,
             "parity": parity,

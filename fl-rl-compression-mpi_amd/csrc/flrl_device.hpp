@@ -126,21 +126,24 @@ __device__ __forceinline__ uint32_t block_excl_scan(const TIn *s_in, uint32_t *s
     return total;
 }
 
-// Decoupled look-back for an additive u64 scan (payload < 2^62). Called by ONE
-// full wave. Publishes the tile's aggregate, accumulates predecessors 64 at a
-// time until it meets an inclusive prefix, publishes its own inclusive prefix
-// and returns the exclusive prefix (to every lane).
-__device__ __noinline__ uint64_t lookback_sum(uint64_t *status, uint32_t tile, uint64_t agg,
-                                              Ctrl *ctrl)
+// Decoupled look-back for an additive u64 scan (payload < 2^62), split in two
+// so a caller can publish its aggregate early and resolve its prefix later.
+// publish_aggregate: ONE lane stores the tile's aggregate (tile 0 publishes its
+// inclusive prefix directly).
+__device__ __forceinline__ void publish_aggregate(uint64_t *status, uint32_t tile, uint64_t agg)
+{
+    granule_store(&status[tile], (tile == 0 ? kFlagP : kFlagA) | agg);
+}
+
+// lookback_resolve: called by ONE full wave after publish_aggregate. Sums
+// predecessors 64 at a time until it meets an inclusive prefix, publishes the
+// tile's inclusive prefix and returns the exclusive prefix (to every lane).
+__device__ __noinline__ uint64_t lookback_resolve(uint64_t *status, uint32_t tile, uint64_t agg,
+                                                  Ctrl *ctrl)
 {
     const int lane = threadIdx.x & (kWave - 1);
-    if (tile == 0) {
-        if (lane == 0)
-            granule_store(&status[0], kFlagP | agg);
+    if (tile == 0)
         return 0;
-    }
-    if (lane == 0)
-        granule_store(&status[tile], kFlagA | agg);
     uint64_t excl = 0;
     int64_t j = (int64_t)tile - 1;
     uint32_t spins = 0;
@@ -168,6 +171,15 @@ __device__ __noinline__ uint64_t lookback_sum(uint64_t *status, uint32_t tile, u
     if (lane == 0)
         granule_store(&status[tile], kFlagP | (excl + agg));
     return excl;
+}
+
+// Both halves in one call (ONE full wave).
+__device__ __forceinline__ uint64_t lookback_sum(uint64_t *status, uint32_t tile, uint64_t agg,
+                                                 Ctrl *ctrl)
+{
+    if ((threadIdx.x & (kWave - 1)) == 0)
+        publish_aggregate(status, tile, agg);
+    return lookback_resolve(status, tile, agg, ctrl);
 }
 
 // 16-byte load of bytes [o, o+16) of p, zero-filling past n.

@@ -9,15 +9,22 @@
 // 16 input bytes <-> 2b output bytes at a position known from a prefix sum of
 // widths — no bit cursor, no atomics on the data path.
 //
-// Encode is a single pass over the input (read once, N+F+V bytes of HBM
-// traffic): each 256-thread workgroup takes a 16*256*ITEMS-byte tile by ticket,
-// keeps it in registers, computes frame widths (OR of the frame's bytes), scans
-// them in LDS, publishes the tile's width sum and resolves its global offset by
-// decoupled look-back while the other waves pack into an LDS staging tile; the
-// packed tile then leaves in coalesced 16-byte stores (offsets are multiples of
-// 16). Decode mirrors it: widths -> scan -> look-back -> the tile's contiguous
-// packed bytes staged into LDS -> each lane unpacks 2b bytes into 16 bytes and
-// stores them coalesced.
+// Encode (fl_encode_kernel) reads the input once (N+F+V bytes of HBM traffic).
+// It is a persistent, software-pipelined kernel: each 256-thread workgroup
+// takes 64 KiB tiles by ticket; for the tile it holds in registers it computes
+// frame widths (OR of the frame's bytes), scans them in LDS and publishes the
+// tile's width sum, then issues the loads of its NEXT tile before resolving the
+// current tile's global offset by decoupled look-back (wave 0) while the other
+// waves pack into an LDS staging tile; the packed tile leaves in coalesced
+// 16-byte stores (offsets are multiples of 16). So HBM loads of tile t+1 are in
+// flight across tile t's look-back, packing and stores.
+//
+// Decode is two launches: fl_offsets_kernel scans the frame widths (F bytes,
+// <1% of the traffic) into per-tile output offsets and validates the widths
+// and valuesSize; fl_decode_kernel is then a pure streaming kernel with no
+// inter-workgroup dependency: each 32 KiB output tile loads its widths and its
+// contiguous packed bytes (16-B aligned) into LDS, unpacks 2b bytes -> 16 bytes
+// per lane and stores coalesced.
 //
 // Replaces the reference kernels compressCalculateOutputBits
 // (fl_gpu.cu:648-685), compressInitializeFrameStartIndiciesBits + thrust scan
@@ -26,7 +33,10 @@
 // reference's 32-bit threadId wraps at 4 GiB, fl_gpu.cu:650,702,730).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
+
+#include <atomic>
 
 #include "flrl.h"
 #include "flrl_device.hpp"
@@ -34,9 +44,15 @@
 
 namespace flrl {
 
-// Tile shape: 256 threads x ITEMS x 16 B. ITEMS = 16 -> 64 KiB tiles (512 frames).
-constexpr int kFlItems = 16;
-constexpr int kFlTileBytes = kThreads * 16 * kFlItems;
+constexpr int kEncItems = 16;  // encode tile = 256 lanes x 16 x 16 B = 64 KiB (512 frames)
+constexpr int kEncTileBytes = kThreads * 16 * kEncItems;
+constexpr int kEncBlocksPerCU = 2;  // LDS 68 KB and ~190 VGPRs per workgroup
+constexpr int kDecItems = 8;   // decode tile = 32 KiB (256 frames)
+constexpr int kDecTileBytes = kThreads * 16 * kDecItems;
+constexpr int kDecTileFrames = kDecTileBytes / kFrame;
+constexpr int kOffFramesPerThread = 64;
+constexpr int kOffFrames = kThreads * kOffFramesPerThread;  // frames per offsets workgroup
+static_assert(kOffFramesPerThread * 4 == kDecTileFrames, "4 offsets lanes per decode tile");
 
 // Pack 8 bytes (each < 2^b) of x into the low 8b bits, value i at bit b*i.
 __device__ __forceinline__ uint64_t pack8(uint64_t x, uint32_t b)
@@ -58,9 +74,29 @@ __device__ __forceinline__ uint64_t unpack8(uint64_t w, uint32_t b)
     return (y & M1) | (((y >> b) & M1) << 8);
 }
 
+__device__ __forceinline__ uint32_t clamp_width(uint32_t b) { return b < 1 ? 1u : (b > 8 ? 8u : b); }
+
 template <int ITEMS>
-__global__ __launch_bounds__(kThreads) void fl_encode_kernel(
-    const uint8_t *__restrict__ in, uint64_t n, uint64_t nframes, uint64_t ntiles,
+__device__ __forceinline__ void load_tile(u32x4 (&v)[ITEMS], const uint8_t *in, uint64_t off,
+                                          uint64_t n)
+{
+    constexpr int TB = kThreads * 16 * ITEMS;
+    const int tid = threadIdx.x;
+    if (off + TB <= n) {
+        const u32x4 *src = reinterpret_cast<const u32x4 *>(in + off);
+#pragma unroll
+        for (int k = 0; k < ITEMS; ++k)
+            v[k] = __builtin_nontemporal_load(src + k * kThreads + tid);
+    } else {
+#pragma unroll
+        for (int k = 0; k < ITEMS; ++k)
+            v[k] = load16_tail(in, off + (uint64_t)(k * kThreads + tid) * 16, n);
+    }
+}
+
+template <int ITEMS>
+__global__ __launch_bounds__(kThreads, kEncBlocksPerCU) void fl_encode_kernel(
+    const uint8_t *__restrict__ in, uint64_t n, uint64_t nframes, uint32_t ntiles,
     uint8_t *__restrict__ bits, uint8_t *__restrict__ values, uint64_t *__restrict__ values_size,
     Ctrl *ctrl, uint64_t *status)
 {
@@ -70,160 +106,240 @@ __global__ __launch_bounds__(kThreads) void fl_encode_kernel(
     __shared__ u32x4 s_w4[TF / 16];
     __shared__ uint32_t s_pref[TF];
     __shared__ uint32_t s_wave[kWaves];
-    __shared__ uint32_t s_ticket;
+    __shared__ uint32_t s_next;
     __shared__ uint64_t s_base;
     uint8_t *s_w = reinterpret_cast<uint8_t *>(s_w4);
+    uint8_t *s_out_b = reinterpret_cast<uint8_t *>(s_out);
 
     const int tid = threadIdx.x;
     const int wave = tid / kWave;
-    const uint32_t tile = take_ticket(ctrl, &s_ticket);
-    const uint64_t tile_off = (uint64_t)tile * TB;
-    const uint64_t frame0 = (uint64_t)tile * TF;
-    const bool full = tile_off + TB <= n;
-
-    // ---- load the tile: 16 B per lane per item, coalesced -----------------
-    u32x4 v[ITEMS];
-    if (full) {
-        const u32x4 *src = reinterpret_cast<const u32x4 *>(in + tile_off);
-#pragma unroll
-        for (int k = 0; k < ITEMS; ++k)
-            v[k] = __builtin_nontemporal_load(src + k * kThreads + tid);
-    } else {
-#pragma unroll
-        for (int k = 0; k < ITEMS; ++k)
-            v[k] = load16_tail(in, tile_off + (uint64_t)(k * kThreads + tid) * 16, n);
-    }
-
-    // ---- frame widths: OR over the frame's 8 lanes, b = max(1, bitlen) ---
-    uint32_t bw[ITEMS];
-#pragma unroll
-    for (int k = 0; k < ITEMS; ++k) {
-        uint32_t o = v[k].x | v[k].y | v[k].z | v[k].w;
-        o |= o >> 16;
-        o |= o >> 8;
-        o &= 0xFFu;
-        o |= __shfl_xor(o, 1, kWave);
-        o |= __shfl_xor(o, 2, kWave);
-        o |= __shfl_xor(o, 4, kWave);
-        uint32_t b = o ? 32u - __clz(o) : 1u;
-        const int ft = k * (kThreads / 8) + (tid >> 3);
-        if (frame0 + ft >= nframes)
-            b = 0;  // past the last frame: contributes nothing
-        bw[k] = b;
-        if ((tid & 7) == 0)
-            s_w[ft] = (uint8_t)b;
-    }
+    if (tid == 0)
+        s_next = atomicAdd(&ctrl->ticket, 1u);
     __syncthreads();
-    const uint32_t agg = block_excl_scan<TF>(s_w, s_pref, s_wave);
-    __syncthreads();
+    uint32_t tile = s_next;
+    if (tile >= ntiles)
+        return;
+    u32x4 a[ITEMS];
+    load_tile<ITEMS>(a, in, (uint64_t)tile * TB, n);
 
-    // ---- bits[] for this tile's frames -----------------------------------
-    if (frame0 + TF <= nframes) {
-        for (int i = tid; i < TF / 16; i += kThreads)
-            reinterpret_cast<u32x4 *>(bits + frame0)[i] = s_w4[i];
-    } else {
-        for (int i = tid; i < TF; i += kThreads)
-            if (frame0 + i < nframes)
-                bits[frame0 + i] = s_w[i];
+    for (;;) {
+        __syncthreads();  // previous tile's LDS readers are done; s_next consumed
+        if (tid == 0)
+            s_next = atomicAdd(&ctrl->ticket, 1u);  // next ticket, read after the barrier below
+        const uint64_t frame0 = (uint64_t)tile * TF;
+
+        // ---- frame widths: OR over the frame's 8 lanes, b = max(1, bitlen)
+        uint32_t bw[ITEMS];
+#pragma unroll
+        for (int k = 0; k < ITEMS; ++k) {
+            uint32_t o = a[k].x | a[k].y | a[k].z | a[k].w;
+            o |= o >> 16;
+            o |= o >> 8;
+            o &= 0xFFu;
+            o |= __shfl_xor(o, 1, kWave);
+            o |= __shfl_xor(o, 2, kWave);
+            o |= __shfl_xor(o, 4, kWave);
+            uint32_t b = o ? 32u - __clz(o) : 1u;
+            const int ft = k * (kThreads / 8) + (tid >> 3);
+            if (frame0 + ft >= nframes)
+                b = 0;  // past the last frame: contributes nothing
+            bw[k] = b;
+            if ((tid & 7) == 0)
+                s_w[ft] = (uint8_t)b;
+        }
+        __syncthreads();
+        const uint32_t nxt = s_next;
+        const uint32_t agg = block_excl_scan<TF>(s_w, s_pref, s_wave);
+        __syncthreads();
+
+        // ---- publish the tile's width sum early (successors' look-backs need it)
+        if (tid == 0)
+            publish_aggregate(status, tile, agg);
+
+        // ---- bits[] for this tile's frames
+        if (frame0 + TF <= nframes) {
+            for (int i = tid; i < TF / 16; i += kThreads)
+                reinterpret_cast<u32x4 *>(bits + frame0)[i] = s_w4[i];
+        } else {
+            for (int i = tid; i < TF; i += kThreads)
+                if (frame0 + i < nframes)
+                    bits[frame0 + i] = s_w[i];
+        }
+
+        // ---- pack each lane's 16 values into 2b bytes of the LDS staging tile
+        // (tile-local offsets: independent of the look-back)
+#pragma unroll
+        for (int k = 0; k < ITEMS; ++k) {
+            const uint32_t w = bw[k];
+            if (w == 0)
+                continue;
+            const int ft = k * (kThreads / 8) + (tid >> 3);
+            const uint32_t off = 16u * s_pref[ft] + 2u * w * (uint32_t)(tid & 7);
+            const uint64_t p0 = pack8(((uint64_t)a[k].y << 32) | a[k].x, w);
+            const uint64_t p1 = pack8(((uint64_t)a[k].w << 32) | a[k].z, w);
+            const uint64_t lo = w == 8 ? p0 : (p0 | (p1 << (8 * w)));
+            const uint64_t hi = w == 8 ? p1 : (p1 >> (64 - 8 * w));
+            uint16_t *d = reinterpret_cast<uint16_t *>(s_out_b + off);
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+                if (i < (int)w)
+                    d[i] = (uint16_t)((i < 4 ? lo >> (16 * i) : hi >> (16 * (i - 4))) & 0xFFFFu);
+        }
+
+        // ---- prefetch the next tile into the now-free registers: its loads are
+        // in flight across this tile's look-back and stores
+        const bool more = nxt < ntiles;
+        if (more)
+            load_tile<ITEMS>(a, in, (uint64_t)nxt * TB, n);
+
+        // ---- wave 0: global offset by look-back
+        if (wave == 0) {
+            const uint64_t excl = lookback_resolve(status, tile, agg, ctrl);
+            if (tid == 0)
+                s_base = excl;
+        }
+        __syncthreads();
+
+        // ---- stream the packed tile out: 16-B aligned, coalesced
+        const uint64_t base = s_base;  // in 16-byte units
+        u32x4 *dst = reinterpret_cast<u32x4 *>(values) + base;
+        if (tile + 1 < ntiles) {
+            for (uint32_t c = tid; c < agg; c += kThreads)
+                __builtin_nontemporal_store(s_out[c], dst + c);
+        } else {
+            // last tile: valuesSize = 16*(frames before last) + ceil(cnt*b_last/8)
+            const int fl = (int)(nframes - 1 - frame0);
+            const uint64_t cnt = n - (nframes - 1) * kFrame;
+            const uint64_t vsize = 16ull * (base + s_pref[fl]) + (cnt * s_w[fl] + 7) / 8;
+            if (tid == 0)
+                *values_size = vsize;
+            for (uint32_t c = tid; c < agg; c += kThreads)
+                store16_tail(values, 16ull * (base + c), vsize, s_out[c]);
+        }
+        if (!more)
+            break;
+        tile = nxt;
     }
+}
 
-    // ---- wave 0: global offset by look-back (overlaps the packing below) --
+// Decode pre-pass: one workgroup scans kOffFrames frame widths (64 per lane),
+// validates them (a width outside [1,8] raises FLRL_E_FORMAT and is clamped, as
+// fl_decode_kernel clamps it, so offsets stay consistent and in bounds), and
+// writes the output offset (16-byte units) of each 256-frame decode tile:
+// tile_base[t] for t < ntiles and tile_base[ntiles] = total. Workgroup offsets
+// come from a decoupled look-back; the workgroup holding the last frame checks
+// valuesSize against the widths.
+__global__ __launch_bounds__(kThreads) void fl_offsets_kernel(
+    const uint8_t *__restrict__ bits, uint64_t nframes, uint64_t vsize, uint64_t n,
+    uint64_t *__restrict__ tile_base, uint32_t ntiles, uint32_t nblocks, Ctrl *ctrl,
+    uint64_t *status)
+{
+    __shared__ uint32_t s_wave[kWaves];
+    __shared__ uint32_t s_ticket;
+    __shared__ uint64_t s_base;
+    const int tid = threadIdx.x;
+    const int lane = tid & (kWave - 1);
+    const int wave = tid / kWave;
+    const uint32_t blk = take_ticket(ctrl, &s_ticket);
+    const uint64_t f0 = (uint64_t)blk * kOffFrames + (uint64_t)tid * kOffFramesPerThread;
+
+    // widths 4 per dword (SWAR): a byte is invalid if it is 0 or > 8
+    uint32_t sum = 0;
+    bool bad = false;
+#pragma unroll
+    for (int q = 0; q < kOffFramesPerThread / 16; ++q) {
+        const uint64_t fq = f0 + 16 * q;
+        if (fq + 16 <= nframes) {
+            const u32x4 w = *reinterpret_cast<const u32x4 *>(bits + fq);
+#pragma unroll
+            for (int d = 0; d < 4; ++d) {
+                const uint32_t x = w[d];
+                const uint32_t zero = (x - 0x01010101u) & ~x & 0x80808080u;
+                const uint32_t big = (((x & 0x7F7F7F7Fu) + 0x77777777u) | x) & 0x80808080u;
+                if (zero | big) {  // rare: clamp byte by byte
+                    bad = true;
+                    for (int i = 0; i < 4; ++i)
+                        sum += clamp_width((x >> (8 * i)) & 0xFFu);
+                } else {
+                    const uint32_t h = (x & 0x00FF00FFu) + ((x >> 8) & 0x00FF00FFu);
+                    sum += (h & 0xFFFFu) + (h >> 16);
+                }
+            }
+        } else {
+            for (int i = 0; i < 16 && fq + i < nframes; ++i) {
+                const uint32_t raw = bits[fq + i];
+                bad |= raw < 1 || raw > 8;
+                sum += clamp_width(raw);
+            }
+        }
+    }
+    if (bad)
+        raise_error(ctrl, FLRL_E_FORMAT);
+
+    // exclusive scan of lane sums over the workgroup
+    const uint32_t inc = wave_incl_scan_u32(sum);
+    if (lane == kWave - 1)
+        s_wave[wave] = inc;
+    __syncthreads();
+    uint32_t before = 0, agg = 0;
+#pragma unroll
+    for (int w = 0; w < kWaves; ++w) {
+        before += w < wave ? s_wave[w] : 0u;
+        agg += s_wave[w];
+    }
+    const uint32_t excl = before + inc - sum;
     if (wave == 0) {
-        const uint64_t excl = lookback_sum(status, tile, agg, ctrl);
+        const uint64_t e = lookback_sum(status, blk, agg, ctrl);
         if (tid == 0)
-            s_base = excl;
-    }
-
-    // ---- pack each lane's 16 values into 2b bytes in the LDS staging tile -
-    uint8_t *s_out_b = reinterpret_cast<uint8_t *>(s_out);
-#pragma unroll
-    for (int k = 0; k < ITEMS; ++k) {
-        const uint32_t b = bw[k];
-        if (b == 0)
-            continue;
-        const int ft = k * (kThreads / 8) + (tid >> 3);
-        const uint32_t off = 16u * s_pref[ft] + 2u * b * (uint32_t)(tid & 7);
-        const uint64_t p0 = pack8(((uint64_t)v[k].y << 32) | v[k].x, b);
-        const uint64_t p1 = pack8(((uint64_t)v[k].w << 32) | v[k].z, b);
-        const uint64_t lo = b == 8 ? p0 : (p0 | (p1 << (8 * b)));
-        const uint64_t hi = b == 8 ? p1 : (p1 >> (64 - 8 * b));
-        uint16_t *d = reinterpret_cast<uint16_t *>(s_out_b + off);
-#pragma unroll
-        for (int i = 0; i < 8; ++i)
-            if (i < (int)b)
-                d[i] = (uint16_t)((i < 4 ? lo >> (16 * i) : hi >> (16 * (i - 4))) & 0xFFFFu);
+            s_base = e;
     }
     __syncthreads();
-
-    // ---- stream the packed tile out: 16-B aligned, coalesced --------------
-    const uint64_t base = s_base;  // in 16-byte units
-    u32x4 *dst = reinterpret_cast<u32x4 *>(values) + base;
-    if (tile + 1 < ntiles) {
-        for (uint32_t c = tid; c < agg; c += kThreads)
-            __builtin_nontemporal_store(s_out[c], dst + c);
-    } else {
-        // last tile: valuesSize = 16*(frames before last) + ceil(cnt*b_last/8)
-        const int fl = (int)(nframes - 1 - frame0);
+    const uint64_t base = s_base;
+    const uint64_t tile = f0 / kDecTileFrames;
+    if ((tid & 3) == 0 && tile < ntiles)
+        tile_base[tile] = base + excl;
+    if (blk + 1 == nblocks && tid == 0)
+        tile_base[ntiles] = base + agg;
+    if (nframes > f0 && nframes <= f0 + kOffFramesPerThread) {  // this lane holds the last frame
+        const uint32_t b_last = clamp_width(bits[nframes - 1]);
         const uint64_t cnt = n - (nframes - 1) * kFrame;
-        const uint64_t vsize = 16ull * (base + s_pref[fl]) + (cnt * s_w[fl] + 7) / 8;
-        if (tid == 0)
-            *values_size = vsize;
-        for (uint32_t c = tid; c < agg; c += kThreads)
-            store16_tail(values, 16ull * (base + c), vsize, s_out[c]);
+        const uint64_t expect = 16ull * (base + excl + sum - b_last) + (cnt * b_last + 7) / 8;
+        if (expect != vsize)
+            raise_error(ctrl, FLRL_E_FORMAT);
     }
 }
 
 template <int ITEMS>
 __global__ __launch_bounds__(kThreads) void fl_decode_kernel(
     const uint8_t *__restrict__ bits, uint64_t nframes, const uint8_t *__restrict__ values,
-    uint64_t vsize, uint8_t *__restrict__ out, uint64_t n, uint64_t ntiles, Ctrl *ctrl,
-    uint64_t *status)
+    uint64_t vsize, uint8_t *__restrict__ out, uint64_t n, const uint64_t *__restrict__ tile_base)
 {
     constexpr int TB = kThreads * 16 * ITEMS;
     constexpr int TF = TB / kFrame;
-    __shared__ u32x4 s_in[TB / 16 + 2];  // +2: a lane may read 4 bytes past its 2b
+    __shared__ u32x4 s_in[TB / 16 + 2];  // +2: a lane may read up to 18 bytes past its frame
     __shared__ u32x4 s_w4[TF / 16];
     __shared__ uint32_t s_pref[TF];
     __shared__ uint32_t s_wave[kWaves];
-    __shared__ uint32_t s_ticket;
-    __shared__ uint64_t s_base;
     uint8_t *s_w = reinterpret_cast<uint8_t *>(s_w4);
 
     const int tid = threadIdx.x;
-    const int wave = tid / kWave;
-    const uint32_t tile = take_ticket(ctrl, &s_ticket);
-    const uint64_t tile_off = (uint64_t)tile * TB;
-    const uint64_t frame0 = (uint64_t)tile * TF;
+    const uint64_t tile = blockIdx.x;
+    const uint64_t tile_off = tile * TB;
+    const uint64_t frame0 = tile * TF;
+    const uint64_t base = tile_base[tile];
+    const uint32_t agg = (uint32_t)(tile_base[tile + 1] - base);
 
-    // ---- widths of this tile's frames, validated to [1,8] -----------------
-    if (frame0 + TF <= nframes) {
-        for (int i = tid; i < TF / 16; i += kThreads)
-            s_w4[i] = reinterpret_cast<const u32x4 *>(bits + frame0)[i];
-    } else {
-        for (int i = tid; i < TF; i += kThreads)
-            s_w[i] = frame0 + i < nframes ? bits[frame0 + i] : 0;
-    }
-    __syncthreads();
-    for (int i = tid; i < TF; i += kThreads) {
-        const uint32_t b = s_w[i];
-        if (frame0 + i < nframes && (b < 1 || b > 8)) {
-            raise_error(ctrl, FLRL_E_FORMAT);
-            s_w[i] = b < 1 ? 1 : 8;
+    // ---- issue the tile's loads: its widths and its packed bytes ---------
+    if (tid < TF / 16) {
+        u32x4 w = load16_tail(bits, frame0 + 16 * tid, nframes);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const uint32_t raw = (w[i >> 2] >> (8 * (i & 3))) & 0xFFu;
+            const uint32_t b = frame0 + 16 * tid + i < nframes ? clamp_width(raw) : 0u;
+            w[i >> 2] = (w[i >> 2] & ~(0xFFu << (8 * (i & 3)))) | (b << (8 * (i & 3)));
         }
+        s_w4[tid] = w;
     }
-    __syncthreads();
-    const uint32_t agg = block_excl_scan<TF>(s_w, s_pref, s_wave);
-    __syncthreads();
-
-    if (wave == 0) {
-        const uint64_t excl = lookback_sum(status, tile, agg, ctrl);
-        if (tid == 0)
-            s_base = excl;
-    }
-    __syncthreads();
-    const uint64_t base = s_base;
-
-    // ---- stage this tile's packed bytes (contiguous, 16-B aligned) --------
     const u32x4 *src = reinterpret_cast<const u32x4 *>(values) + base;
     if (16ull * (base + agg) <= vsize) {
         for (uint32_t c = tid; c < agg; c += kThreads)
@@ -234,13 +350,8 @@ __global__ __launch_bounds__(kThreads) void fl_decode_kernel(
     }
     if (tid < 2)
         s_in[agg + tid] = u32x4{0u, 0u, 0u, 0u};
-    if (tile + 1 == ntiles && tid == 0) {
-        const int fl = (int)(nframes - 1 - frame0);
-        const uint64_t cnt = n - (nframes - 1) * kFrame;
-        const uint64_t expect = 16ull * (base + s_pref[fl]) + (cnt * s_w[fl] + 7) / 8;
-        if (expect != vsize)
-            raise_error(ctrl, FLRL_E_FORMAT);
-    }
+    __syncthreads();
+    block_excl_scan<TF>(s_w, s_pref, s_wave);
     __syncthreads();
 
     // ---- unpack 2b bytes -> 16 values per lane, store coalesced -----------
@@ -276,16 +387,50 @@ __global__ __launch_bounds__(kThreads) void fl_decode_kernel(
     }
 }
 
-static size_t fl_tiles(size_t n) { return div_up(n, (size_t)kFlTileBytes); }
+// ---- scratch layout ---------------------------------------------------------
+// [Ctrl 16 B][encode: status[enc_tiles]]   or
+// [Ctrl 16 B][decode: status[off_blocks] (16-B padded)][tile_base[dec_tiles + 1]]
+// Only Ctrl + status are zeroed per call.
+struct FlLayout {
+    size_t enc_tiles, dec_tiles, off_blocks;
+    size_t enc_zero, dec_zero, bytes;
+    explicit FlLayout(size_t n)
+    {
+        const size_t frames = div_up(n, kFrame);
+        enc_tiles = div_up(n, (size_t)kEncTileBytes);
+        dec_tiles = div_up(n, (size_t)kDecTileBytes);
+        off_blocks = div_up(frames, (size_t)kOffFrames);
+        enc_zero = sizeof(Ctrl) + round_up(enc_tiles * 8, 16);
+        dec_zero = sizeof(Ctrl) + round_up(off_blocks * 8, 16);
+        const size_t dec_bytes = dec_zero + round_up((dec_tiles + 1) * 8, 16);
+        bytes = enc_zero > dec_bytes ? enc_zero : dec_bytes;
+    }
+};
+
+static int cu_count()
+{
+    static std::atomic<int> cache[64];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess)
+        dev = 0;
+    if (dev >= 0 && dev < 64) {
+        const int c = cache[dev].load(std::memory_order_relaxed);
+        if (c > 0)
+            return c;
+    }
+    int c = 0;
+    if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c <= 0)
+        c = 256;
+    if (dev >= 0 && dev < 64)
+        cache[dev].store(c, std::memory_order_relaxed);
+    return c;
+}
 
 }  // namespace flrl
 
 using namespace flrl;
 
-extern "C" size_t flrl_fl_scratch_bytes(size_t n)
-{
-    return sizeof(Ctrl) + round_up(fl_tiles(n) * sizeof(uint64_t), 16);
-}
+extern "C" size_t flrl_fl_scratch_bytes(size_t n) { return FlLayout(n).bytes; }
 
 extern "C" size_t flrl_fl_values_capacity(size_t n) { return round_up(n ? n : 1, 16); }
 
@@ -294,15 +439,16 @@ extern "C" int flrl_fl_encode_device(const uint8_t *d_in, size_t n, uint8_t *d_b
                                      size_t scratch_bytes, void *stream)
 {
     hipStream_t s = static_cast<hipStream_t>(stream);
+    const FlLayout L(n);
     if (!d_values_size || !d_scratch)
         return set_error(FLRL_E_ARG, "flrl_fl_encode_device: null values_size/scratch");
-    if (scratch_bytes < flrl_fl_scratch_bytes(n))
+    if (scratch_bytes < L.bytes)
         return set_error(FLRL_E_ARG, "flrl_fl_encode_device: scratch %zu < required %zu",
-                         scratch_bytes, flrl_fl_scratch_bytes(n));
+                         scratch_bytes, L.bytes);
     if (!aligned16(d_scratch))
         return set_error(FLRL_E_ARG, "flrl_fl_encode_device: scratch not 16-byte aligned");
-    FLRL_HIP(hipMemsetAsync(d_scratch, 0, flrl_fl_scratch_bytes(n), s));
     if (n == 0) {
+        FLRL_HIP(hipMemsetAsync(d_scratch, 0, sizeof(Ctrl), s));
         FLRL_HIP(hipMemsetAsync(d_values_size, 0, sizeof(uint64_t), s));
         return FLRL_OK;
     }
@@ -310,13 +456,15 @@ extern "C" int flrl_fl_encode_device(const uint8_t *d_in, size_t n, uint8_t *d_b
         return set_error(FLRL_E_ARG, "flrl_fl_encode_device: null buffer");
     if (!aligned16(d_in) || !aligned16(d_bits) || !aligned16(d_values))
         return set_error(FLRL_E_ARG, "flrl_fl_encode_device: buffers must be 16-byte aligned");
-    const size_t tiles = fl_tiles(n);
-    if (tiles > 0xFFFFFFFFull)
+    if (L.enc_tiles > 0xFFFFFFFFull)
         return set_error(FLRL_E_ARG, "flrl_fl_encode_device: input too large");
+    FLRL_HIP(hipMemsetAsync(d_scratch, 0, L.enc_zero, s));
     Ctrl *ctrl = static_cast<Ctrl *>(d_scratch);
     uint64_t *status = reinterpret_cast<uint64_t *>(ctrl + 1);
-    hipLaunchKernelGGL(fl_encode_kernel<kFlItems>, dim3((uint32_t)tiles), dim3(kThreads), 0, s,
-                       d_in, (uint64_t)n, (uint64_t)div_up(n, kFrame), (uint64_t)tiles, d_bits,
+    const size_t resident = (size_t)kEncBlocksPerCU * cu_count();
+    const uint32_t grid = (uint32_t)(L.enc_tiles < resident ? L.enc_tiles : resident);
+    hipLaunchKernelGGL(fl_encode_kernel<kEncItems>, dim3(grid), dim3(kThreads), 0, s, d_in,
+                       (uint64_t)n, (uint64_t)div_up(n, kFrame), (uint32_t)L.enc_tiles, d_bits,
                        d_values, d_values_size, ctrl, status);
     FLRL_HIP(hipGetLastError());
     return FLRL_OK;
@@ -327,30 +475,38 @@ extern "C" int flrl_fl_decode_device(const uint8_t *d_bits, size_t bits_size,
                                      size_t n, void *d_scratch, size_t scratch_bytes, void *stream)
 {
     hipStream_t s = static_cast<hipStream_t>(stream);
+    const FlLayout L(n);
     if (!d_scratch)
         return set_error(FLRL_E_ARG, "flrl_fl_decode_device: null scratch");
-    if (scratch_bytes < flrl_fl_scratch_bytes(n))
+    if (scratch_bytes < L.bytes)
         return set_error(FLRL_E_ARG, "flrl_fl_decode_device: scratch %zu < required %zu",
-                         scratch_bytes, flrl_fl_scratch_bytes(n));
+                         scratch_bytes, L.bytes);
     if (!aligned16(d_scratch))
         return set_error(FLRL_E_ARG, "flrl_fl_decode_device: scratch not 16-byte aligned");
-    FLRL_HIP(hipMemsetAsync(d_scratch, 0, flrl_fl_scratch_bytes(n), s));
-    if (n == 0)
+    if (n == 0) {
+        FLRL_HIP(hipMemsetAsync(d_scratch, 0, sizeof(Ctrl), s));
         return FLRL_OK;
+    }
     if (bits_size != div_up(n, kFrame))
         return set_error(FLRL_E_FORMAT, "bitsSize %zu != ceil(%zu/128)", bits_size, n);
     if (!d_bits || !d_values || !d_out)
         return set_error(FLRL_E_ARG, "flrl_fl_decode_device: null buffer");
     if (!aligned16(d_bits) || !aligned16(d_values) || !aligned16(d_out))
         return set_error(FLRL_E_ARG, "flrl_fl_decode_device: buffers must be 16-byte aligned");
-    const size_t tiles = fl_tiles(n);
-    if (tiles > 0xFFFFFFFFull)
+    if (L.dec_tiles > 0x7FFFFFFFull)
         return set_error(FLRL_E_ARG, "flrl_fl_decode_device: output too large");
+    FLRL_HIP(hipMemsetAsync(d_scratch, 0, L.dec_zero, s));
     Ctrl *ctrl = static_cast<Ctrl *>(d_scratch);
     uint64_t *status = reinterpret_cast<uint64_t *>(ctrl + 1);
-    hipLaunchKernelGGL(fl_decode_kernel<kFlItems>, dim3((uint32_t)tiles), dim3(kThreads), 0, s,
-                       d_bits, (uint64_t)bits_size, d_values, (uint64_t)values_size, d_out,
-                       (uint64_t)n, (uint64_t)tiles, ctrl, status);
+    uint64_t *tile_base =
+        reinterpret_cast<uint64_t *>(static_cast<uint8_t *>(d_scratch) + L.dec_zero);
+    hipLaunchKernelGGL(fl_offsets_kernel, dim3((uint32_t)L.off_blocks), dim3(kThreads), 0, s,
+                       d_bits, (uint64_t)bits_size, (uint64_t)values_size, (uint64_t)n, tile_base,
+                       (uint32_t)L.dec_tiles, (uint32_t)L.off_blocks, ctrl, status);
+    FLRL_HIP(hipGetLastError());
+    hipLaunchKernelGGL(fl_decode_kernel<kDecItems>, dim3((uint32_t)L.dec_tiles), dim3(kThreads), 0,
+                       s, d_bits, (uint64_t)bits_size, d_values, (uint64_t)values_size, d_out,
+                       (uint64_t)n, tile_base);
     FLRL_HIP(hipGetLastError());
     return FLRL_OK;
 }
