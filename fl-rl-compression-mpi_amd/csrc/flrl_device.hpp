@@ -73,6 +73,16 @@ __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v)
     return v;
 }
 
+// OR across each aligned group of 8 lanes with DPP (no LDS crossbar):
+// quad_perm [1,0,3,2], quad_perm [2,3,0,1], then row_half_mirror (lane i <-> 7-i).
+__device__ __forceinline__ uint32_t or_8lanes(uint32_t o)
+{
+    o |= (uint32_t)__builtin_amdgcn_mov_dpp((int)o, 0xB1, 0xF, 0xF, false);
+    o |= (uint32_t)__builtin_amdgcn_mov_dpp((int)o, 0x4E, 0xF, 0xF, false);
+    o |= (uint32_t)__builtin_amdgcn_mov_dpp((int)o, 0x141, 0xF, 0xF, false);
+    return o;
+}
+
 __device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t v)
 {
     const int lane = threadIdx.x & (kWave - 1);
@@ -86,13 +96,15 @@ __device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t v)
 }
 
 // Exclusive scan of N small counts held in LDS (s_in, any integer type) into
-// s_out. Returns the total to every thread. Requires N % 256 == 0 or N < 256.
-// Caller must __syncthreads() before reading s_out and before reusing s_wave.
-template <int N, typename TIn>
+// s_out by a T-thread block. Returns the total to every thread. Requires
+// N % T == 0 or N < T. Caller must __syncthreads() before reading s_out and
+// before reusing s_wave (T/64 words).
+template <int N, typename TIn, int T = kThreads>
 __device__ __forceinline__ uint32_t block_excl_scan(const TIn *s_in, uint32_t *s_out,
                                                     uint32_t *s_wave)
 {
-    constexpr int E = N >= kThreads ? N / kThreads : 1;
+    constexpr int E = N >= T ? N / T : 1;
+    constexpr int kWaves = T / kWave;
     const int tid = threadIdx.x;
     const int lane = tid & (kWave - 1);
     const int wave = tid / kWave;
@@ -126,6 +138,19 @@ __device__ __forceinline__ uint32_t block_excl_scan(const TIn *s_in, uint32_t *s
     return total;
 }
 
+// A look-back window (lane i holds the status of tile j-i) is usable once every
+// slot up to and including the nearest inclusive prefix (P) is published; slots
+// beyond that P are not needed, so a straggler further back never stalls us.
+__device__ __forceinline__ bool window_ready(uint64_t s)
+{
+    const unsigned long long xm = __ballot((s >> 62) == 0);
+    const unsigned long long pm = __ballot((s >> 62) == 2);
+    if (!pm)
+        return xm == 0;
+    const unsigned long long upto = pm & (~pm + 1);  // lowest P lane
+    return (xm & ((upto << 1) - 1)) == 0;
+}
+
 // Decoupled look-back for an additive u64 scan (payload < 2^62), split in two
 // so a caller can publish its aggregate early and resolve its prefix later.
 // publish_aggregate: ONE lane stores the tile's aggregate (tile 0 publishes its
@@ -138,7 +163,9 @@ __device__ __forceinline__ void publish_aggregate(uint64_t *status, uint32_t til
 // lookback_resolve: called by ONE full wave after publish_aggregate. Sums
 // predecessors 64 at a time until it meets an inclusive prefix, publishes the
 // tile's inclusive prefix and returns the exclusive prefix (to every lane).
-__device__ __noinline__ uint64_t lookback_resolve(uint64_t *status, uint32_t tile, uint64_t agg,
+// Must stay inlined: a call makes the callee open with s_waitcnt vmcnt(0),
+// which would drain the caller's in-flight prefetch loads before the look-back.
+__device__ __forceinline__ uint64_t lookback_resolve(uint64_t *status, uint32_t tile, uint64_t agg,
                                                   Ctrl *ctrl)
 {
     const int lane = threadIdx.x & (kWave - 1);
@@ -152,7 +179,7 @@ __device__ __noinline__ uint64_t lookback_resolve(uint64_t *status, uint32_t til
         uint64_t s;
         for (;;) {
             s = idx >= 0 ? granule_load(&status[idx]) : kFlagP;
-            if (!__any((s >> 62) == 0))
+            if (window_ready(s))
                 break;
             if (++spins > kSpinLimit) {
                 if (lane == 0)
@@ -173,6 +200,45 @@ __device__ __noinline__ uint64_t lookback_resolve(uint64_t *status, uint32_t til
     return excl;
 }
 
+// As lookback_resolve, but the first window (tiles tile-1-lane) was already
+// loaded by the caller into `probe` — issue that load early (before long
+// streams of other vector-memory ops) so its wait does not queue behind them.
+__device__ __forceinline__ uint64_t lookback_resolve_probed(uint64_t *status, uint32_t tile,
+                                                            uint64_t agg, Ctrl *ctrl,
+                                                            uint64_t probe)
+{
+    const int lane = threadIdx.x & (kWave - 1);
+    if (tile == 0)
+        return 0;
+    uint64_t excl = 0;
+    int64_t j = (int64_t)tile - 1;
+    uint32_t spins = 0;
+    uint64_t s = probe;
+    for (;;) {
+        const int64_t idx = j - lane;
+        while (!window_ready(s)) {
+            if (++spins > kSpinLimit) {
+                if (lane == 0)
+                    raise_error(ctrl, FLRL_E_TIMEOUT);
+                return excl;
+            }
+            __builtin_amdgcn_s_sleep(1);
+            s = idx >= 0 ? granule_load(&status[idx]) : kFlagP;
+        }
+        const unsigned long long pm = __ballot((s >> 62) == 2);
+        const int first_p = pm ? __ffsll(pm) - 1 : kWave;
+        excl += wave_sum_u64(lane <= first_p ? (s & kPayload) : 0ull);
+        if (pm)
+            break;
+        j -= kWave;
+        const int64_t nidx = j - lane;
+        s = nidx >= 0 ? granule_load(&status[nidx]) : kFlagP;
+    }
+    if (lane == 0)
+        granule_store(&status[tile], kFlagP | (excl + agg));
+    return excl;
+}
+
 // Both halves in one call (ONE full wave).
 __device__ __forceinline__ uint64_t lookback_sum(uint64_t *status, uint32_t tile, uint64_t agg,
                                                  Ctrl *ctrl)
@@ -182,17 +248,23 @@ __device__ __forceinline__ uint64_t lookback_sum(uint64_t *status, uint32_t tile
     return lookback_resolve(status, tile, agg, ctrl);
 }
 
-// 16-byte load of bytes [o, o+16) of p, zero-filling past n.
+// 16-byte load of bytes [o, o+16) of p (o and p 16-byte aligned), zero-filling
+// past n. A straddling chunk is read whole: a 16-byte-aligned block never
+// crosses a page, so this cannot fault; the bytes at or past n are masked off.
 __device__ __forceinline__ u32x4 load16_tail(const uint8_t *p, uint64_t o, uint64_t n)
 {
-    if (o + 16 <= n)
-        return *reinterpret_cast<const u32x4 *>(p + o);
-    uint32_t w[4] = {0u, 0u, 0u, 0u};
+    if (o >= n)
+        return u32x4{0u, 0u, 0u, 0u};
+    u32x4 v = *reinterpret_cast<const u32x4 *>(p + o);
+    if (o + 16 > n) {
+        const uint32_t r = (uint32_t)(n - o);  // 1..15 valid bytes
 #pragma unroll
-    for (int i = 0; i < 16; ++i)
-        if (o + i < n)
-            w[i >> 2] |= (uint32_t)p[o + i] << (8 * (i & 3));
-    return u32x4{w[0], w[1], w[2], w[3]};
+        for (int d = 0; d < 4; ++d) {
+            const uint32_t keep = r >= 4u * (d + 1) ? 4u : (r > 4u * d ? r - 4u * d : 0u);
+            v[d] &= keep >= 4 ? 0xFFFFFFFFu : ((1u << (8 * keep)) - 1u);
+        }
+    }
+    return v;
 }
 
 // 16-byte store of v to bytes [o, o+16) of p, dropping bytes at or past n.
@@ -202,11 +274,10 @@ __device__ __forceinline__ void store16_tail(uint8_t *p, uint64_t o, uint64_t n,
         *reinterpret_cast<u32x4 *>(p + o) = v;
         return;
     }
-    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-    for (int i = 0; i < 16; ++i)
-        if (o + i < n)
-            p[o + i] = (uint8_t)(w[i >> 2] >> (8 * (i & 3)));
+    const uint64_t lo = ((uint64_t)v.y << 32) | v.x, hi = ((uint64_t)v.w << 32) | v.z;
+#pragma unroll 1
+    for (uint32_t i = 0; i < 16 && o + i < n; ++i)
+        p[o + i] = (uint8_t)(i < 8 ? lo >> (8 * i) : hi >> (8 * (i - 8)));
 }
 
 }  // namespace flrl

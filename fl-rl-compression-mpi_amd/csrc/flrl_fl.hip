@@ -10,14 +10,16 @@
 // widths — no bit cursor, no atomics on the data path.
 //
 // Encode (fl_encode_kernel) reads the input once (N+F+V bytes of HBM traffic).
-// It is a persistent, software-pipelined kernel: each 256-thread workgroup
-// takes 64 KiB tiles by ticket; for the tile it holds in registers it computes
-// frame widths (OR of the frame's bytes), scans them in LDS and publishes the
-// tile's width sum, then issues the loads of its NEXT tile before resolving the
-// current tile's global offset by decoupled look-back (wave 0) while the other
-// waves pack into an LDS staging tile; the packed tile leaves in coalesced
-// 16-byte stores (offsets are multiples of 16). So HBM loads of tile t+1 are in
-// flight across tile t's look-back, packing and stores.
+// It is a persistent, software-pipelined kernel with one 512-thread workgroup
+// per CU taking 128 KiB tiles by ticket: for the tile it holds in registers it
+// computes frame widths (OR of the frame's bytes), scans them in LDS, publishes
+// the tile's width sum and packs into an LDS staging tile; then it issues the
+// loads of its NEXT tile, resolves the current tile's global offset by
+// decoupled look-back (wave 0) and streams the packed tile out in coalesced
+// 16-byte stores (offsets are multiples of 16). HBM loads of tile t+1 are in
+// flight across tile t's look-back and stores. Tile size, workgroup shape and
+// the look-back ordering were chosen by measurement (scripts/ubench_encode.hip,
+// DESIGN.md §Encode).
 //
 // Decode is two launches: fl_offsets_kernel scans the frame widths (F bytes,
 // <1% of the traffic) into per-tile output offsets and validates the widths
@@ -44,9 +46,9 @@
 
 namespace flrl {
 
-constexpr int kEncItems = 16;  // encode tile = 256 lanes x 16 x 16 B = 64 KiB (512 frames)
-constexpr int kEncTileBytes = kThreads * 16 * kEncItems;
-constexpr int kEncBlocksPerCU = 2;  // LDS 68 KB and ~190 VGPRs per workgroup
+constexpr int kEncThreads = 512;  // encode workgroup: 8 waves, one per CU (LDS 133 KB)
+constexpr int kEncItems = 16;     // encode tile = 512 lanes x 16 x 16 B = 128 KiB (1024 frames)
+constexpr int kEncTileBytes = kEncThreads * 16 * kEncItems;
 constexpr int kDecItems = 8;   // decode tile = 32 KiB (256 frames)
 constexpr int kDecTileBytes = kThreads * 16 * kDecItems;
 constexpr int kDecTileFrames = kDecTileBytes / kFrame;
@@ -76,36 +78,72 @@ __device__ __forceinline__ uint64_t unpack8(uint64_t w, uint32_t b)
 
 __device__ __forceinline__ uint32_t clamp_width(uint32_t b) { return b < 1 ? 1u : (b > 8 ? 8u : b); }
 
-template <int ITEMS>
+template <int T, int ITEMS>
 __device__ __forceinline__ void load_tile(u32x4 (&v)[ITEMS], const uint8_t *in, uint64_t off,
                                           uint64_t n)
 {
-    constexpr int TB = kThreads * 16 * ITEMS;
+    constexpr int TB = T * 16 * ITEMS;
     const int tid = threadIdx.x;
     if (off + TB <= n) {
         const u32x4 *src = reinterpret_cast<const u32x4 *>(in + off);
 #pragma unroll
         for (int k = 0; k < ITEMS; ++k)
-            v[k] = __builtin_nontemporal_load(src + k * kThreads + tid);
+            v[k] = __builtin_nontemporal_load(src + k * T + tid);
     } else {
 #pragma unroll
         for (int k = 0; k < ITEMS; ++k)
-            v[k] = load16_tail(in, off + (uint64_t)(k * kThreads + tid) * 16, n);
+            v[k] = load16_tail(in, off + (uint64_t)(k * T + tid) * 16, n);
     }
 }
 
-template <int ITEMS>
-__global__ __launch_bounds__(kThreads, kEncBlocksPerCU) void fl_encode_kernel(
+// Write a lane's 2b packed bytes (lo = bytes 0-7, hi = bytes 8-15) to LDS at
+// byte offset off = 16*pref + 2b*j with the widest store the alignment of 2b*j
+// allows: b = 8 -> one 16-B store, b = 4 -> 8 B, b = 2 or 6 -> dwords, odd b ->
+// 16-bit stores.
+__device__ __forceinline__ void stage_packed(uint8_t *s, uint32_t off, uint32_t b, uint64_t lo,
+                                             uint64_t hi)
+{
+    if (b == 8) {
+        *reinterpret_cast<u32x4 *>(s + off) =
+            u32x4{(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)};
+    } else if (b == 4) {
+        *reinterpret_cast<uint64_t *>(s + off) = lo;
+    } else if ((b & 1) == 0) {  // 2 or 6
+        uint32_t *d = reinterpret_cast<uint32_t *>(s + off);
+        d[0] = (uint32_t)lo;
+        if (b == 6) {
+            d[1] = (uint32_t)(lo >> 32);
+            d[2] = (uint32_t)hi;
+        }
+    } else {
+        uint16_t *d = reinterpret_cast<uint16_t *>(s + off);
+#pragma unroll
+        for (int i = 0; i < 7; ++i)
+            if (i < (int)b)
+                d[i] = (uint16_t)((i < 4 ? lo >> (16 * i) : hi >> (16 * (i - 4))) & 0xFFFFu);
+    }
+}
+
+// FL encode: persistent, one T-thread workgroup per CU, 16*T*ITEMS-byte tiles
+// (128 KiB at T = 512, ITEMS = 16) taken by ticket. Per tile: widths (OR of
+// each frame's 8 lanes), LDS scan, publish the width sum, pack into the LDS
+// staging tile, prefetch the next tile into the freed registers, resolve the
+// tile's offset by look-back (wave 0), stream the staged bytes out. Wave 0
+// issues its share of the prefetch only after its look-back: vmcnt is per wave
+// and in order, so status loads issued behind 16 bulk loads would each wait
+// for all of them (measured: scripts/ubench_encode.hip).
+template <int T, int ITEMS>
+__global__ __launch_bounds__(T, 1) void fl_encode_kernel(
     const uint8_t *__restrict__ in, uint64_t n, uint64_t nframes, uint32_t ntiles,
     uint8_t *__restrict__ bits, uint8_t *__restrict__ values, uint64_t *__restrict__ values_size,
     Ctrl *ctrl, uint64_t *status)
 {
-    constexpr int TB = kThreads * 16 * ITEMS;
+    constexpr int TB = T * 16 * ITEMS;
     constexpr int TF = TB / kFrame;
     __shared__ u32x4 s_out[TB / 16];
     __shared__ u32x4 s_w4[TF / 16];
     __shared__ uint32_t s_pref[TF];
-    __shared__ uint32_t s_wave[kWaves];
+    __shared__ uint32_t s_wave[T / kWave];
     __shared__ uint32_t s_next;
     __shared__ uint64_t s_base;
     uint8_t *s_w = reinterpret_cast<uint8_t *>(s_w4);
@@ -120,7 +158,7 @@ __global__ __launch_bounds__(kThreads, kEncBlocksPerCU) void fl_encode_kernel(
     if (tile >= ntiles)
         return;
     u32x4 a[ITEMS];
-    load_tile<ITEMS>(a, in, (uint64_t)tile * TB, n);
+    load_tile<T, ITEMS>(a, in, (uint64_t)tile * TB, n);
 
     for (;;) {
         __syncthreads();  // previous tile's LDS readers are done; s_next consumed
@@ -135,12 +173,9 @@ __global__ __launch_bounds__(kThreads, kEncBlocksPerCU) void fl_encode_kernel(
             uint32_t o = a[k].x | a[k].y | a[k].z | a[k].w;
             o |= o >> 16;
             o |= o >> 8;
-            o &= 0xFFu;
-            o |= __shfl_xor(o, 1, kWave);
-            o |= __shfl_xor(o, 2, kWave);
-            o |= __shfl_xor(o, 4, kWave);
+            o = or_8lanes(o & 0xFFu);
             uint32_t b = o ? 32u - __clz(o) : 1u;
-            const int ft = k * (kThreads / 8) + (tid >> 3);
+            const int ft = k * (T / 8) + (tid >> 3);
             if (frame0 + ft >= nframes)
                 b = 0;  // past the last frame: contributes nothing
             bw[k] = b;
@@ -149,7 +184,7 @@ __global__ __launch_bounds__(kThreads, kEncBlocksPerCU) void fl_encode_kernel(
         }
         __syncthreads();
         const uint32_t nxt = s_next;
-        const uint32_t agg = block_excl_scan<TF>(s_w, s_pref, s_wave);
+        const uint32_t agg = block_excl_scan<TF, uint8_t, T>(s_w, s_pref, s_wave);
         __syncthreads();
 
         // ---- publish the tile's width sum early (successors' look-backs need it)
@@ -158,45 +193,43 @@ __global__ __launch_bounds__(kThreads, kEncBlocksPerCU) void fl_encode_kernel(
 
         // ---- bits[] for this tile's frames
         if (frame0 + TF <= nframes) {
-            for (int i = tid; i < TF / 16; i += kThreads)
+            for (int i = tid; i < TF / 16; i += T)
                 reinterpret_cast<u32x4 *>(bits + frame0)[i] = s_w4[i];
         } else {
-            for (int i = tid; i < TF; i += kThreads)
+            for (int i = tid; i < TF; i += T)
                 if (frame0 + i < nframes)
                     bits[frame0 + i] = s_w[i];
         }
 
-        // ---- pack each lane's 16 values into 2b bytes of the LDS staging tile
-        // (tile-local offsets: independent of the look-back)
+        // ---- pack 16 values -> 2b bytes per lane into the LDS staging tile
 #pragma unroll
         for (int k = 0; k < ITEMS; ++k) {
-            const uint32_t w = bw[k];
-            if (w == 0)
+            const uint32_t b = bw[k];
+            if (b == 0)
                 continue;
-            const int ft = k * (kThreads / 8) + (tid >> 3);
-            const uint32_t off = 16u * s_pref[ft] + 2u * w * (uint32_t)(tid & 7);
-            const uint64_t p0 = pack8(((uint64_t)a[k].y << 32) | a[k].x, w);
-            const uint64_t p1 = pack8(((uint64_t)a[k].w << 32) | a[k].z, w);
-            const uint64_t lo = w == 8 ? p0 : (p0 | (p1 << (8 * w)));
-            const uint64_t hi = w == 8 ? p1 : (p1 >> (64 - 8 * w));
-            uint16_t *d = reinterpret_cast<uint16_t *>(s_out_b + off);
-#pragma unroll
-            for (int i = 0; i < 8; ++i)
-                if (i < (int)w)
-                    d[i] = (uint16_t)((i < 4 ? lo >> (16 * i) : hi >> (16 * (i - 4))) & 0xFFFFu);
+            const int ft = k * (T / 8) + (tid >> 3);
+            const uint32_t off = 16u * s_pref[ft] + 2u * b * (uint32_t)(tid & 7);
+            const uint64_t x0 = ((uint64_t)a[k].y << 32) | a[k].x;
+            const uint64_t x1 = ((uint64_t)a[k].w << 32) | a[k].z;
+            uint64_t lo = x0, hi = x1;
+            if (b != 8) {
+                const uint64_t p0 = pack8(x0, b), p1 = pack8(x1, b);
+                lo = p0 | (p1 << (8 * b));
+                hi = p1 >> (64 - 8 * b);
+            }
+            stage_packed(s_out_b, off, b, lo, hi);
         }
 
-        // ---- prefetch the next tile into the now-free registers: its loads are
-        // in flight across this tile's look-back and stores
+        // ---- prefetch the next tile into the freed registers (wave 0: later)
         const bool more = nxt < ntiles;
-        if (more)
-            load_tile<ITEMS>(a, in, (uint64_t)nxt * TB, n);
-
-        // ---- wave 0: global offset by look-back
+        if (more && wave != 0)
+            load_tile<T, ITEMS>(a, in, (uint64_t)nxt * TB, n);
         if (wave == 0) {
             const uint64_t excl = lookback_resolve(status, tile, agg, ctrl);
             if (tid == 0)
                 s_base = excl;
+            if (more)
+                load_tile<T, ITEMS>(a, in, (uint64_t)nxt * TB, n);
         }
         __syncthreads();
 
@@ -204,8 +237,14 @@ __global__ __launch_bounds__(kThreads, kEncBlocksPerCU) void fl_encode_kernel(
         const uint64_t base = s_base;  // in 16-byte units
         u32x4 *dst = reinterpret_cast<u32x4 *>(values) + base;
         if (tile + 1 < ntiles) {
-            for (uint32_t c = tid; c < agg; c += kThreads)
-                __builtin_nontemporal_store(s_out[c], dst + c);
+            u32x4 o[ITEMS];  // static trip count: LDS reads hoisted, stores predicated
+#pragma unroll
+            for (int k = 0; k < ITEMS; ++k)
+                o[k] = s_out[k * T + tid];
+#pragma unroll
+            for (int k = 0; k < ITEMS; ++k)
+                if ((uint32_t)(k * T + tid) < agg)
+                    __builtin_nontemporal_store(o[k], dst + k * T + tid);
         } else {
             // last tile: valuesSize = 16*(frames before last) + ceil(cnt*b_last/8)
             const int fl = (int)(nframes - 1 - frame0);
@@ -213,7 +252,7 @@ __global__ __launch_bounds__(kThreads, kEncBlocksPerCU) void fl_encode_kernel(
             const uint64_t vsize = 16ull * (base + s_pref[fl]) + (cnt * s_w[fl] + 7) / 8;
             if (tid == 0)
                 *values_size = vsize;
-            for (uint32_t c = tid; c < agg; c += kThreads)
+            for (uint32_t c = tid; c < agg; c += T)
                 store16_tail(values, 16ull * (base + c), vsize, s_out[c]);
         }
         if (!more)
@@ -461,9 +500,10 @@ extern "C" int flrl_fl_encode_device(const uint8_t *d_in, size_t n, uint8_t *d_b
     FLRL_HIP(hipMemsetAsync(d_scratch, 0, L.enc_zero, s));
     Ctrl *ctrl = static_cast<Ctrl *>(d_scratch);
     uint64_t *status = reinterpret_cast<uint64_t *>(ctrl + 1);
-    const size_t resident = (size_t)kEncBlocksPerCU * cu_count();
+    const size_t resident = (size_t)cu_count();
     const uint32_t grid = (uint32_t)(L.enc_tiles < resident ? L.enc_tiles : resident);
-    hipLaunchKernelGGL(fl_encode_kernel<kEncItems>, dim3(grid), dim3(kThreads), 0, s, d_in,
+    hipLaunchKernelGGL((fl_encode_kernel<kEncThreads, kEncItems>), dim3(grid), dim3(kEncThreads), 0,
+                       s, d_in,
                        (uint64_t)n, (uint64_t)div_up(n, kFrame), (uint32_t)L.enc_tiles, d_bits,
                        d_values, d_values_size, ctrl, status);
     FLRL_HIP(hipGetLastError());
