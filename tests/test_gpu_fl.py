@@ -257,3 +257,16 @@ def test_cli_gpu_methods(golden, bmp_bytes, cli_path, tmp_path):
         subprocess.run([cli_path, "d", method, str(out), str(back)], check=True,
                        capture_output=True)
         assert back.read_bytes() == bmp_bytes
+
+
+def test_cli_rl_gpu(bmp_bytes, cli_path, tmp_path):
+    src = tmp_path / "in.bmp"
+    src.write_bytes(bmp_bytes)
+    subprocess.run([cli_path, "c", "rl", str(src), str(tmp_path / "o.rl")], check=True,
+                   capture_output=True)
+    subprocess.run([cli_path, "c", "rl-cpu", str(src), str(tmp_path / "o2.rl")], check=True,
+                   capture_output=True)
+    assert (tmp_path / "o.rl").read_bytes() == (tmp_path / "o2.rl").read_bytes()
+    subprocess.run([cli_path, "d", "rl", str(tmp_path / "o.rl"), str(tmp_path / "b")], check=True,
+                   capture_output=True)
+    assert (tmp_path / "b").read_bytes() == bmp_bytes

@@ -1,0 +1,126 @@
+"""RL parity on the MI355X: HIP path (through the C ABI) vs the CPU oracle.
+
+The reference fork has no RL code, so the oracle is the
+restatement of IMPLEMENTATION-PLAN.md:81-179, pinned only by the plan's worked
+examples (tests/golden/golden.json "rl_kat"): RL parity is partially unpinned.
+Bit-exact checks cover runs crossing 16-byte lanes, 1 KiB wave items, 16 KiB
+wave sub-tiles and 128 KiB tiles, 255-splits of long runs starting anywhere
+(including inside earlier tiles), and config #3 (1 GiB runs32) in full.
+"""
+import numpy as np
+import pytest
+
+import flrl
+import oracle
+from conftest import kat_input
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available() or flrl.device_count() == 0:
+        pytest.fail("GPU tests need a HIP device")
+
+
+def check(a: np.ndarray):
+    r = flrl.rl_compress(a)
+    counts, values = oracle.rl_compress(a)
+    assert r.input_size == a.size
+    assert r.counts.size == counts.size, (r.counts.size, counts.size)
+    assert np.array_equal(r.counts, counts)
+    assert np.array_equal(r.values, values)
+    back = flrl.rl_decompress(a.size, r.counts, r.values)
+    assert np.array_equal(back, a)
+    return r
+
+
+def test_kats(golden):
+    for case in golden["rl_kat"]:
+        data = np.frombuffer(kat_input(case), np.uint8)
+        r = flrl.rl_compress(data)
+        assert r.counts.tolist() == case["counts"], case["name"]
+        assert r.values.tolist() == case["values"], case["name"]
+        assert flrl.rl_decompress(data.size, r.counts, r.values).tobytes() == data.tobytes()
+
+
+def test_empty():
+    r = flrl.rl_compress(b"")
+    assert r.counts.size == 0 and r.input_size == 0
+    assert flrl.rl_decompress(0, r.counts, r.values).size == 0
+
+
+SIZES = [1, 2, 15, 16, 17, 255, 256, 257, 1023, 1024, 1025, 16383, 16384, 16385,
+         131071, 131072, 131073, 300_001, (1 << 20) + 7]
+
+
+@pytest.mark.parametrize("n", SIZES)
+@pytest.mark.parametrize("kind", ["runs32", "longruns", "u8", "zero"])
+def test_sizes_vs_oracle(n, kind):
+    check(oracle.gen(kind, n, 17))
+
+
+@pytest.mark.parametrize("L", [254, 255, 256, 509, 510, 511, 16384 + 3, 131072 + 255, 400_000])
+@pytest.mark.parametrize("start", [0, 1, 15, 16, 1023, 16380, 131070])
+def test_long_run_splits(L, start):
+    # one long run of 7s starting at `start` inside random data
+    rng = np.random.default_rng(L + start)
+    a = rng.integers(0, 256, size=start + L + 300, dtype=np.uint8)
+    a[start:start + L] = 7
+    if start > 0 and a[start - 1] == 7:
+        a[start - 1] = 8
+    if a[start + L] == 7:
+        a[start + L] = 9
+    check(a)
+
+
+def test_runs_spanning_many_tiles():
+    # alternating long runs of 1..3 tiles, so most tiles have no natural head
+    parts = []
+    rng = np.random.default_rng(3)
+    v = 0
+    total = 0
+    while total < 3_000_000:
+        L = int(rng.integers(1, 3 * 131072))
+        parts.append(np.full(L, v, np.uint8))
+        v = (v + 1 + int(rng.integers(0, 200))) % 256
+        total += L
+    check(np.concatenate(parts))
+
+
+def test_all_zero_large():
+    a = np.zeros(5 * 131072 + 77, np.uint8)  # no natural head after byte 0
+    r = check(a)
+    assert r.counts.tolist()[:3] == [255, 255, 255]
+
+
+def test_decode_rejects_malformed():
+    with pytest.raises(flrl.FLRLError) as e:
+        flrl.rl_decompress(5, np.array([2, 0, 3], np.uint8), np.array([1, 2, 3], np.uint8))
+    assert e.value.code == flrl.E_FORMAT
+    with pytest.raises(flrl.FLRLError):
+        flrl.rl_decompress(6, np.array([2, 3], np.uint8), np.array([1, 2], np.uint8))
+    with pytest.raises(flrl.FLRLError):
+        flrl.rl_decompress(3, np.zeros(0, np.uint8), np.zeros(0, np.uint8))
+
+
+def test_device_1gib_runs32():
+    """Config #3: RL encode/decode of 1 GiB runs32 (mean run 32) — bit-exact vs
+    the oracle over the full buffer and a device round trip."""
+    from flrl.device import RLDevice
+    n = 1 << 30
+    a = oracle.gen("runs32", n, 42)
+    counts, values = oracle.rl_compress(a)
+    x = torch.from_numpy(a).cuda()
+    d = RLDevice(n)
+    d.encode(x)
+    R = d.runs()
+    assert d.error() == 0
+    assert R == counts.size
+    assert np.array_equal(d.counts[:R].cpu().numpy(), counts)
+    assert np.array_equal(d.values[:R].cpu().numpy(), values)
+    out = d.decode(R)
+    assert d.error() == 0
+    assert torch.equal(out, x)
