@@ -33,7 +33,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 import flrl  # noqa: E402
-from flrl.device import FLDevice, gen  # noqa: E402
+from flrl.device import FLDevice, RLDevice, gen  # noqa: E402
 from flrl.dist import size_scan  # noqa: E402
 
 METRIC = ("encode+decode GB/s (input bytes) at 1/2/4/8 GPUs; % HBM roofline; "
@@ -53,6 +53,8 @@ def parse():
     p.add_argument("--cpu-sample", type=int, default=-1,
                    help="bytes of the workload the CPU oracle times (default: min(bytes, 1 GiB)); 0 = skip")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"))
+    p.add_argument("--no-rl", action="store_true",
+                   help="skip the RL section (config #3: 1 GiB runs32), which runs at N=1 only")
     return p.parse_args()
 
 
@@ -93,6 +95,65 @@ def cpu_baseline(kind: str, seed: int, sample: int, gpu_bits, gpu_values):
         "roundtrip_ok": ok,
         "gpu_bytes_equal_oracle": same,
     }
+
+
+def rl_section(n: int, seed: int, steps: int, warmup: int, dev, cpu: bool):
+    """BASELINE configs[2]: RL encode/decode of n bytes of runs32 (mean run 32).
+    Input generated on the host by the product generator (runs32 is
+    sequential), copied to HBM before timing."""
+    x = torch.from_numpy(flrl.gen_host("runs32", n, seed)).to(dev)
+    d = RLDevice(n, dev)
+    stream = torch.cuda.current_stream()
+    d.encode(x)
+    R = d.runs()
+    out = d.decode(R)
+    ok = bool(torch.equal(out, x)) and d.error() == 0
+    for _ in range(warmup):
+        d.encode(x)
+        d.decode(R)
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(steps)]
+    torch.cuda.synchronize()
+    for k in range(steps):
+        ev[k][0].record(stream)
+        d.encode(x)
+        ev[k][1].record(stream)
+        d.decode(R)
+        ev[k][2].record(stream)
+    torch.cuda.synchronize()
+    assert d.error() == 0
+    enc_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in ev]))
+    dec_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in ev]))
+    alg = n + 2 * R  # SURVEY.md §8(d): RL encode N+2R, decode 2R+N
+    res = {
+        "workload": f"RL encode+decode of {n} bytes runs32 (seed {seed}), BASELINE configs[2]",
+        "runs": R,
+        "value": round(n / ((enc_ms + dec_ms) * 1e-3) / 1e9, 2),
+        "unit": "GB/s (input bytes, encode+decode)",
+        "rl_encode": {"ms": round(enc_ms, 4), "alg_GBps": round(alg / (enc_ms * 1e-3) / 1e9, 1),
+                      "frac": round(alg / (enc_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
+        "rl_decode": {"ms": round(dec_ms, 4), "alg_GBps": round(alg / (dec_ms * 1e-3) / 1e9, 1),
+                      "frac": round(alg / (dec_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
+        "roundtrip": ok,
+    }
+    if cpu:
+        import oracle
+        a = x.cpu().numpy()
+        t0 = time.perf_counter()
+        counts, values = oracle.rl_compress(a)
+        t1 = time.perf_counter()
+        back = oracle.rl_decompress(counts, values, n)
+        t2 = time.perf_counter()
+        same = bool(counts.size == R and np.array_equal(d.counts[:R].cpu().numpy(), counts)
+                    and np.array_equal(d.values[:R].cpu().numpy(), values))
+        res["cpu_baseline"] = {
+            "value": round(n / (t2 - t0) / 1e9, 4), "unit": "GB/s", "cores": 1, "kind": "port",
+            "sample": f"the full {n}-byte runs32 input; oracle rl encode {t1 - t0:.2f} s + "
+                      f"decode {t2 - t1:.2f} s, single-threaded",
+            "roundtrip_ok": bool(np.array_equal(back, a)), "gpu_bytes_equal_oracle": same,
+        }
+    del x, d, out
+    torch.cuda.empty_cache()
+    return res
 
 
 def main():
@@ -206,6 +267,9 @@ def main():
         sample = min(n, 1 << 30) if args.cpu_sample < 0 else args.cpu_sample
         if world == 1 and sample > 0:
             cpu = cpu_baseline(args.kind, args.seed, sample, gpu_bits, gpu_values)
+        rl = None
+        if world == 1 and not args.no_rl:
+            rl = rl_section(n, args.seed, args.steps, args.warmup, dev, cpu=sample > 0)
         line = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -248,6 +312,7 @@ def main():
             },
             "cpu_baseline": cpu,
             "parity": parity,
+            "rl": rl,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

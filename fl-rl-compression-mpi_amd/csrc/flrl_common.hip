@@ -83,3 +83,49 @@ extern "C" int flrl_gen_device(int kind, uint64_t seed, uint64_t word_offset, ui
     FLRL_HIP(hipGetLastError());
     return FLRL_OK;
 }
+
+static uint64_t splitmix_next(uint64_t *state)
+{
+    uint64_t z = (*state += 0x9E3779B97F4A7C15ull);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+extern "C" int flrl_gen_host(int kind, uint64_t seed, uint64_t word_offset, uint8_t *out, size_t n)
+{
+    if (n && !out)
+        return set_error(FLRL_E_ARG, "flrl_gen_host: null output");
+    if (kind >= 0 && kind <= 2) {
+        const uint8_t mask = kind == 0 ? 0xFF : (kind == 1 ? 0x0F : 0x00);
+        for (size_t w = 0; w * 8 < n; ++w) {
+            uint64_t st = seed + (word_offset + w) * 0x9E3779B97F4A7C15ull;
+            const uint64_t word = splitmix_next(&st);
+            for (size_t j = 0; j < 8 && w * 8 + j < n; ++j)
+                out[w * 8 + j] = (uint8_t)((word >> (8 * j)) & mask);
+        }
+        return FLRL_OK;
+    }
+    if (kind == 3 || kind == 4) {
+        if (word_offset != 0)
+            return set_error(FLRL_E_ARG, "flrl_gen_host: run kinds are sequential (word_offset 0)");
+        const uint64_t mod = kind == 3 ? 63 : 1023;
+        uint64_t st = seed;
+        size_t i = 0;
+        uint8_t prev = 0;
+        while (i < n) {
+            const uint64_t r = splitmix_next(&st);
+            size_t len = (size_t)(1 + r % mod);
+            uint8_t val = (uint8_t)((r >> 32) & 0xFF);
+            if (i > 0 && val == prev)
+                val ^= 0x80;
+            if (len > n - i)
+                len = n - i;
+            memset(out + i, val, len);
+            i += len;
+            prev = val;
+        }
+        return FLRL_OK;
+    }
+    return set_error(FLRL_E_ARG, "flrl_gen_host: unknown kind %d", kind);
+}

@@ -110,6 +110,7 @@ _sig("flrl_rl_encode_device", ctypes.c_int, _vp, _sz, _vp, _vp, _vp, _vp, _sz, _
 _sig("flrl_rl_decode_scratch_bytes", _sz, _sz)
 _sig("flrl_rl_decode_device", ctypes.c_int, _vp, _vp, _sz, _vp, _sz, _vp, _sz, _vp)
 _sig("flrl_gen_device", ctypes.c_int, ctypes.c_int, _u64, _u64, _vp, _sz, _vp)
+_sig("flrl_gen_host", ctypes.c_int, ctypes.c_int, _u64, _u64, _vp, _sz)
 
 _libc = ctypes.CDLL(None)
 _libc.free.argtypes = [_vp]
@@ -261,6 +262,14 @@ def rl_decode_device(d_counts: int, d_values: int, runs: int, d_out: int, n: int
 def gen_device(kind, seed: int, word_offset: int, d_out: int, n: int, stream: int = 0) -> None:
     k = GEN_KINDS[kind] if isinstance(kind, str) else int(kind)
     _check(_lib.flrl_gen_device(k, seed, word_offset, d_out, n, stream or None))
+
+
+def gen_host(kind, n: int, seed: int, word_offset: int = 0) -> np.ndarray:
+    """SURVEY.md §8(d) synthetic input on the host (all kinds, incl. runs32)."""
+    k = GEN_KINDS[kind] if isinstance(kind, str) else int(kind)
+    out = np.empty(n, dtype=np.uint8)
+    _check(_lib.flrl_gen_host(k, seed, word_offset, out.ctypes.data if n else None, n))
+    return out
 
 
 def scratch_error(d_scratch: int, stream: int = 0) -> int:

@@ -140,6 +140,11 @@ int flrl_rl_decode_device(const uint8_t *d_counts, const uint8_t *d_values, size
 int flrl_gen_device(int kind, uint64_t seed, uint64_t word_offset, uint8_t *d_out, size_t n,
                     void *stream);
 
+/* Same generator on the host, all kinds: 0 u8, 1 lo4, 2 zero (word_offset as
+ * above), 3 runs32 (runs of 1..63 equal bytes), 4 longruns (runs of 1..1023);
+ * the run kinds are sequential and need word_offset == 0. */
+int flrl_gen_host(int kind, uint64_t seed, uint64_t word_offset, uint8_t *out, size_t n);
+
 #ifdef __cplusplus
 }
 #endif
