@@ -21,10 +21,10 @@
 //
 // Decode: rl_offsets_kernel scans the counts (R bytes) into per-tile output
 // offsets (and validates them); rl_decode_kernel then expands each tile of
-// runs independently: 16-byte output chunks, each located by a binary search
-// of the tile's count prefix in LDS, filled run by run and stored (interior
-// chunks as dwordx4; the two boundary chunks a tile shares with its
-// neighbours byte by byte).
+// 4096 runs independently, in 32 KiB LDS output windows: the runs overlapping
+// a window memset their bytes into it with aligned dword stores, and the window
+// leaves in 16-byte stores (the two chunks a tile shares with its neighbours
+// byte by byte).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdlib.h>
@@ -41,8 +41,9 @@ constexpr int kRlItems = 16;                         // 16 x 16 B per lane
 constexpr int kRlWaveBytes = kWave * 16 * kRlItems;  // 16 KiB per wave (contiguous)
 constexpr int kRlTileBytes = kRlWaveBytes * (kRlThreads / kWave);  // 128 KiB
 
-constexpr int kRdRuns = 8192;        // runs per decode tile
+constexpr int kRdRuns = 4096;        // runs per decode tile
 constexpr int kRdThreads = 256;
+constexpr int kRdWindow = 32768;     // LDS output window (bytes)
 constexpr int kRoRunsPerThread = 256;
 constexpr int kRoRuns = kRoRunsPerThread * kThreads;  // runs per offsets workgroup
 static_assert(kRdRuns % kRoRunsPerThread == 0, "whole offsets lanes per decode tile");
@@ -409,14 +410,36 @@ __global__ __launch_bounds__(kThreads) void rl_offsets_kernel(
 }
 
 // ---- decode: expand one tile of kRdRuns runs ------------------------------
+// The tile's output [base, end) is produced in kRdWindow-byte windows aligned to
+// global 16-byte boundaries: the runs overlapping a window (one binary search
+// of the count prefix per window) memset their bytes into an LDS window with
+// aligned dword stores, then the window leaves in 16-byte stores (the two
+// chunks a tile shares with its neighbours byte by byte).
+__device__ __forceinline__ uint32_t run_lower(const uint32_t *pre, uint32_t nr, uint32_t x)
+{
+    // last j in [0, nr) with pre[j] <= x (pre[0] = 0 <= x)
+    uint32_t a = 0, b = nr;
+    while (b - a > 1) {
+        const uint32_t m = (a + b) >> 1;
+        if (pre[m] <= x)
+            a = m;
+        else
+            b = m;
+    }
+    return a;
+}
+
 __global__ __launch_bounds__(kRdThreads) void rl_decode_kernel(
     const uint8_t *__restrict__ counts, const uint8_t *__restrict__ values, uint64_t runs,
     uint8_t *__restrict__ out, uint64_t n, const uint64_t *__restrict__ tile_base)
 {
     __shared__ uint32_t s_pre[kRdRuns + 1];  // local output offset of each run
     __shared__ u32x4 s_val4[kRdRuns / 16];
+    __shared__ u32x4 s_win4[kRdWindow / 16];
     __shared__ uint32_t s_wave[kRdThreads / kWave];
     uint8_t *s_val = reinterpret_cast<uint8_t *>(s_val4);
+    uint8_t *s_win = reinterpret_cast<uint8_t *>(s_win4);
+    uint32_t *s_win32 = reinterpret_cast<uint32_t *>(s_win4);
     const int tid = threadIdx.x;
     const int lane = tid & (kWave - 1);
     const int wave = tid / kWave;
@@ -424,19 +447,19 @@ __global__ __launch_bounds__(kRdThreads) void rl_decode_kernel(
     const uint64_t r0 = tile * kRdRuns;
     const uint64_t base = tile_base[tile];
     const uint64_t end = tile_base[tile + 1];
-    if (end > n || base > end)
-        return;  // malformed (flagged by rl_offsets_kernel)
+    if (end > n || base >= end)
+        return;  // empty, or malformed (flagged by rl_offsets_kernel)
     const uint32_t nr = (uint32_t)(runs - r0 < (uint64_t)kRdRuns ? runs - r0 : kRdRuns);
 
-    // counts -> per-thread sums (32 runs per thread) -> block scan -> s_pre
-    constexpr int RPT = kRdRuns / kRdThreads;  // 32
+    // ---- counts -> block scan -> s_pre; values -> LDS ------------------------
+    constexpr int RPT = kRdRuns / kRdThreads;
+    static_assert(RPT % 16 == 0, "whole 16-byte count vectors per thread");
     uint32_t c[RPT];
     uint32_t sum = 0;
 #pragma unroll
     for (int q = 0; q < RPT / 16; ++q) {
         const u32x4 v = load16_tail(counts, r0 + tid * RPT + 16 * q, runs);
-        const u32x4 vv = load16_tail(values, r0 + tid * RPT + 16 * q, runs);
-        s_val4[(tid * RPT) / 16 + q] = vv;
+        s_val4[(tid * RPT) / 16 + q] = load16_tail(values, r0 + tid * RPT + 16 * q, runs);
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
             c[16 * q + i] = (v[i >> 2] >> (8 * (i & 3))) & 0xFFu;
@@ -461,50 +484,44 @@ __global__ __launch_bounds__(kRdThreads) void rl_decode_kernel(
         s_pre[kRdRuns] = (uint32_t)(end - base);
     __syncthreads();
 
-    // 16-byte output chunks overlapping [base, end)
-    const uint64_t q0 = base / 16, q1 = (end + 15) / 16;
-    const uint32_t total = (uint32_t)(end - base);
-    for (uint64_t q = q0 + tid; q < q1; q += kRdThreads) {
-        const uint64_t p0 = q * 16;
-        const uint32_t lo = p0 > base ? (uint32_t)(p0 - base) : 0u;  // first local byte
-        const uint32_t skip = p0 < base ? (uint32_t)(base - p0) : 0u;  // bytes before the tile
-        // run containing local byte lo: last j with s_pre[j] <= lo
-        uint32_t a = 0, b = nr;  // invariant: s_pre[a] <= lo < s_pre[b]
-        while (b - a > 1) {
-            const uint32_t m = (a + b) >> 1;
-            if (s_pre[m] <= lo)
-                a = m;
-            else
-                b = m;
-        }
-        uint64_t wlo = 0, whi = 0;
-        uint32_t pos = lo, j = a;
-        for (uint32_t f = skip; f < 16 && pos < total; ) {
-            const uint32_t run_end = j + 1 <= nr ? (j + 1 == nr ? total : s_pre[j + 1]) : total;
-            uint32_t take = run_end - pos;
-            if (take > 16 - f)
-                take = 16 - f;
-            const uint64_t v = s_val[j] * 0x0101010101010101ull;
-            for (uint32_t t = 0; t < take; ++t, ++f) {
-                if (f < 8)
-                    wlo |= (v & 0xFFull) << (8 * f);
-                else
-                    whi |= (v & 0xFFull) << (8 * (f - 8));
+    // ---- windows ---------------------------------------------------------------
+    const uint64_t g0 = base & ~15ull;
+    for (uint64_t gw = g0; gw < end; gw += kRdWindow) {
+        const uint32_t lo = (uint32_t)((gw > base ? gw : base) - base);  // owned, tile-local
+        const uint32_t hi = (uint32_t)((gw + kRdWindow < end ? gw + kRdWindow : end) - base);
+        const uint32_t shift = (uint32_t)(gw < base ? base - gw : 0);    // window pos of local lo
+        const uint32_t ja = run_lower(s_pre, nr, lo);
+        const uint32_t jb = run_lower(s_pre, nr, hi - 1) + 1;
+        for (uint32_t j = ja + tid; j < jb; j += kRdThreads) {
+            uint32_t x = s_pre[j], y = j + 1 < nr ? s_pre[j + 1] : hi;
+            x = x < lo ? lo : x;
+            y = y > hi ? hi : y;
+            if (x >= y)
+                continue;
+            // window positions [x - lo + shift, y - lo + shift)
+            uint32_t p = x - lo + shift, q = y - lo + shift;
+            const uint32_t v = s_val[j];
+            while (p < q && (p & 3)) s_win[p++] = (uint8_t)v;
+            const uint32_t v4 = v * 0x01010101u;
+            while (p + 4 <= q) {
+                s_win32[p >> 2] = v4;
+                p += 4;
             }
-            pos += take;
-            ++j;
+            while (p < q) s_win[p++] = (uint8_t)v;
         }
-        const u32x4 r = u32x4{(uint32_t)wlo, (uint32_t)(wlo >> 32), (uint32_t)whi,
-                              (uint32_t)(whi >> 32)};
-        if (p0 >= base && p0 + 16 <= end) {
-            __builtin_nontemporal_store(r, reinterpret_cast<u32x4 *>(out + p0));
-        } else {
-            for (uint32_t f = 0; f < 16; ++f) {
-                const uint64_t p = p0 + f;
-                if (p >= base && p < end)
-                    out[p] = (uint8_t)(f < 8 ? wlo >> (8 * f) : whi >> (8 * (f - 8)));
+        __syncthreads();
+        const uint32_t wlen = (uint32_t)(end - gw < (uint64_t)kRdWindow ? end - gw : kRdWindow);
+        for (uint32_t ch = tid; ch * 16 < wlen; ch += kRdThreads) {
+            const uint64_t gp = gw + 16ull * ch;
+            if (gp >= base && gp + 16 <= end) {
+                __builtin_nontemporal_store(s_win4[ch], reinterpret_cast<u32x4 *>(out + gp));
+            } else {
+                for (uint32_t f = 0; f < 16; ++f)
+                    if (gp + f >= base && gp + f < end)
+                        out[gp + f] = s_win[16 * ch + f];
             }
         }
+        __syncthreads();
     }
 }
 
