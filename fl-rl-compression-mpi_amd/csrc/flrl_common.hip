@@ -129,3 +129,15 @@ extern "C" int flrl_gen_host(int kind, uint64_t seed, uint64_t word_offset, uint
     }
     return set_error(FLRL_E_ARG, "flrl_gen_host: unknown kind %d", kind);
 }
+
+// Error word of a device call (Ctrl::error in the scratch area; FL and RL).
+extern "C" int flrl_scratch_error(const void *d_scratch, void *stream)
+{
+    if (!d_scratch)
+        return set_error(FLRL_E_ARG, "flrl_scratch_error: null scratch");
+    Ctrl c;
+    FLRL_HIP(hipMemcpyAsync(&c, d_scratch, sizeof(c), hipMemcpyDeviceToHost,
+                            static_cast<hipStream_t>(stream)));
+    FLRL_HIP(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
+    return (int)c.error;
+}

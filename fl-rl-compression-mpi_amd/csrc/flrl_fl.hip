@@ -551,17 +551,6 @@ extern "C" int flrl_fl_decode_device(const uint8_t *d_bits, size_t bits_size,
     return FLRL_OK;
 }
 
-extern "C" int flrl_scratch_error(const void *d_scratch, void *stream)
-{
-    if (!d_scratch)
-        return set_error(FLRL_E_ARG, "flrl_scratch_error: null scratch");
-    Ctrl c;
-    FLRL_HIP(hipMemcpyAsync(&c, d_scratch, sizeof(c), hipMemcpyDeviceToHost,
-                            static_cast<hipStream_t>(stream)));
-    FLRL_HIP(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
-    return (int)c.error;
-}
-
 // ---------------------------------------------------------------------------
 // Host-buffer entry points (synchronous), mirroring gpuCompress/gpuDecompress.
 // ---------------------------------------------------------------------------

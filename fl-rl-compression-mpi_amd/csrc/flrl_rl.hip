@@ -9,15 +9,16 @@
 // predecessor (or is byte 0). The state c before a byte is the number of bytes
 // of the current chunk so far (1..254, with 255 written as 0); byte i is a head
 // iff it is natural or c == 0, and then c becomes 1, else c = (c+1) mod 255.
-// A segment of L bytes acts on c as a PhaseMap: a constant (if it contains a
-// natural head: c after it depends only on its last natural head) or
-// "+L mod 255" — maps compose associatively, so the chunk state at every byte
-// comes from an exclusive scan of maps (lanes -> waves -> tiles, the last by a
-// decoupled look-back). With c known, head counts are local; a second,
-// additive look-back gives each tile its first output index. Each head h
-// emits the run that ENDS at h-1 (count = c before h, value = x[h-1]); the
-// tile holding byte n-1 emits the final run. So no tile ever needs bytes of
-// its successor.
+// Within a tile, a PhaseMap scan (constant after a natural head, else
+// "+L mod 255") gives every lane's state relative to the tile's incoming one.
+// Across tiles ONE decoupled look-back composes segment maps {bytes before the
+// first natural head, heads from it on, state after} into (heads before the
+// tile, state at its start). Each head h emits the run that ENDS at h-1
+// (count = c before h, value = x[h-1]); the tile holding byte n-1 emits the
+// final run, so no tile needs bytes of its successor. Heads from a tile's first
+// natural head on do not depend on the incoming state: their runs are staged
+// in LDS before the look-back, and only the split heads before that first
+// natural head (all full 255-byte chunks) wait for it.
 //
 // Decode: rl_offsets_kernel scans the counts (R bytes) into per-tile output
 // offsets (and validates them); rl_decode_kernel then expands each tile of
@@ -34,12 +35,20 @@
 #include "flrl_device.hpp"
 #include "flrl_internal.hpp"
 
+// Phase-timing hooks for scripts/ubench_rl.hip (no-ops in the library).
+#ifndef FLRL_RL_PHASE
+#define FLRL_RL_PHASE_BEGIN() ((void)0)
+#define FLRL_RL_PHASE(k) ((void)0)
+#define FLRL_RL_PHASE_END() ((void)0)
+#endif
+
 namespace flrl {
 
-constexpr int kRlThreads = 512;                      // encode workgroup: 8 waves
+constexpr int kRlThreads = 256;                      // encode workgroup: 4 waves
 constexpr int kRlItems = 16;                         // 16 x 16 B per lane
 constexpr int kRlWaveBytes = kWave * 16 * kRlItems;  // 16 KiB per wave (contiguous)
-constexpr int kRlTileBytes = kRlWaveBytes * (kRlThreads / kWave);  // 128 KiB
+constexpr int kRlTileBytes = kRlWaveBytes * (kRlThreads / kWave);  // 64 KiB
+constexpr int kRlStage = 16384;  // runs per tile staged in LDS (2 x 16 KiB)
 
 constexpr int kRdRuns = 4096;        // runs per decode tile
 constexpr int kRdThreads = 256;
@@ -82,63 +91,6 @@ __device__ __forceinline__ uint32_t wave_incl_scan_map(uint32_t m)
     return m;
 }
 
-// Look-back over PhaseMaps: status granule payload = map (9 bits). A published
-// constant map (A with a natural head) or an inclusive P stops the walk.
-// Returns the chunk state c at the tile start; publishes the tile's P.
-__device__ __forceinline__ uint32_t lookback_phase(uint64_t *status, uint32_t tile, uint32_t map,
-                                                   Ctrl *ctrl)
-{
-    const int lane = threadIdx.x & (kWave - 1);
-    if (tile == 0) {
-        if (lane == 0)
-            granule_store(&status[0], kFlagP | pm_apply(map, 0) | 0x100u);
-        return 0;
-    }
-    uint32_t acc = kMapIdent;  // composition of the maps walked so far (nearest last)
-    int64_t j = (int64_t)tile - 1;
-    uint32_t spins = 0;
-    uint32_t c_in = 0;
-    for (;;) {
-        const int64_t idx = j - lane;
-        uint64_t s;
-        bool done = false;
-        for (;;) {
-            s = idx >= 0 ? granule_load(&status[idx]) : (kFlagP | 0x100u);
-            const unsigned long long xm = __ballot((s >> 62) == 0);
-            const unsigned long long stop = __ballot((s >> 62) == 2 || (s & 0x100u));
-            const unsigned long long upto = stop ? (stop & (~stop + 1)) : 0;
-            if (stop ? (xm & ((upto << 1) - 1)) == 0 : xm == 0)
-                break;
-            if (++spins > kSpinLimit) {
-                if (lane == 0)
-                    raise_error(ctrl, FLRL_E_TIMEOUT);
-                return 0;
-            }
-            __builtin_amdgcn_s_sleep(1);
-        }
-        const unsigned long long stop = __ballot((s >> 62) == 2 || (s & 0x100u));
-        const int first = stop ? __ffsll(stop) - 1 : kWave;
-        // compose lanes first..0 (oldest first) onto acc (which is newer)
-        uint32_t m = lane <= first ? (uint32_t)(s & 0x1FFu) : kMapIdent;
-        // lane order is newest (0) to oldest (63): inclusive scan from high lanes
-        // down = compose(older, newer). Do it serially in lane 0 for clarity.
-        uint32_t win = kMapIdent;
-        for (int l = (first < kWave ? first : kWave - 1); l >= 0; --l)
-            win = pm_compose(win, __shfl(m, l, kWave));
-        acc = pm_compose(win, acc);
-        if (stop) {
-            c_in = pm_apply(acc, 0);  // acc starts with a constant map
-            done = true;
-        }
-        if (done)
-            break;
-        j -= kWave;
-    }
-    if (lane == 0)
-        granule_store(&status[tile], kFlagP | 0x100u | pm_apply(map, c_in));
-    return c_in;
-}
-
 // 16-bit mask of bytes of x that differ from their predecessor (p = byte before).
 __device__ __forceinline__ uint32_t nat_mask(u32x4 x, uint32_t p)
 {
@@ -161,28 +113,242 @@ __device__ __forceinline__ uint32_t byte_at(u32x4 x, uint32_t i)
     return (uint32_t)((i < 8 ? lo >> (8 * i) : hi >> (8 * (i - 8))) & 0xFFu);
 }
 
-template <int T, int ITEMS>
+// ---- composite segment map for the single tile look-back -------------------
+// Acting on the state (H = heads before, c = chunk state) at a segment start:
+//   kind NoNat (L):       H += splits(c, L);        c = (c + L) mod 255
+//   kind Nat (pre, K, ca): H += splits(c, pre) + K;  c = ca
+//   kind Const (H, c):    the state itself (an inclusive prefix)
+// splits(c, m) = #{j < m : (c + j) mod 255 == 0}. Packed in 56 bits: c in 0-7,
+// pre/L in 8-30, K in 31-53, kind in 54-55; Const keeps H in bits 8-53.
+constexpr uint64_t kSmNat = 1ull << 54, kSmConst = 2ull << 54, kSmKind = 3ull << 54;
+__device__ __forceinline__ uint64_t sm_nonat(uint32_t L) { return (uint64_t)L << 8; }
+__device__ __forceinline__ uint64_t sm_nat(uint32_t pre, uint32_t K, uint32_t c)
+{
+    return kSmNat | ((uint64_t)K << 31) | ((uint64_t)pre << 8) | c;
+}
+__device__ __forceinline__ uint64_t sm_const(uint64_t H, uint32_t c) { return kSmConst | (H << 8) | c; }
+__device__ __forceinline__ uint32_t sm_c(uint64_t m) { return (uint32_t)(m & 0xFFu); }
+__device__ __forceinline__ uint32_t sm_a(uint64_t m) { return (uint32_t)(m >> 8) & 0x7FFFFFu; }
+__device__ __forceinline__ uint32_t sm_b(uint64_t m) { return (uint32_t)(m >> 31) & 0x7FFFFFu; }
+__device__ __forceinline__ uint64_t sm_h(uint64_t m) { return (m >> 8) & ((1ull << 46) - 1); }
+// 32-bit forms for packed (< 2^23) lengths; the 64-bit ones only for the
+// cross-window accumulator of the look-back
+__device__ __forceinline__ uint32_t splits(uint32_t c, uint32_t m)
+{
+    const uint32_t j0 = c == 0 ? 0 : 255 - c;
+    return m > j0 ? 1 + (m - 1 - j0) / 255 : 0;
+}
+__device__ __forceinline__ uint32_t add_c(uint32_t c, uint32_t L) { return (c + L) % 255; }
+__device__ __forceinline__ uint64_t splits64(uint32_t c, uint64_t m)
+{
+    const uint64_t j0 = c == 0 ? 0 : 255 - c;
+    return m > j0 ? 1 + (m - 1 - j0) / 255 : 0;
+}
+__device__ __forceinline__ uint32_t add_c64(uint32_t c, uint64_t L) { return (uint32_t)((c + L) % 255); }
+// a then b. Const appears only as the oldest operand.
+__device__ __forceinline__ uint64_t sm_compose(uint64_t a, uint64_t b)
+{
+    const uint64_t kb = b & kSmKind, ka = a & kSmKind;
+    if (kb == kSmConst)
+        return b;
+    if (ka == kSmConst) {
+        const uint64_t H = sm_h(a);
+        const uint32_t c = sm_c(a);
+        if (kb == kSmNat)
+            return sm_const(H + splits(c, sm_a(b)) + sm_b(b), sm_c(b));
+        return sm_const(H + splits(c, sm_a(b)), add_c(c, sm_a(b)));
+    }
+    if (kb == kSmNat) {
+        if (ka == kSmNat)
+            return sm_nat(sm_a(a), sm_b(a) + splits(sm_c(a), sm_a(b)) + sm_b(b), sm_c(b));
+        return sm_nat(sm_a(a) + sm_a(b), sm_b(b), sm_c(b));
+    }
+    if (ka == kSmNat)
+        return sm_nat(sm_a(a), sm_b(a) + splits(sm_c(a), sm_a(b)), add_c(sm_c(a), sm_a(b)));
+    return sm_nonat(sm_a(a) + sm_a(b));
+}
+
+// Look-back for (H, c), run by ONE wave after the tile published its composite
+// map (A; tile 0 publishes its inclusive prefix P instead): compose the window
+// from the nearest P forward (6-level shuffle tree), publish this tile's P,
+// return the Const state at the tile start. Windows hold <= 64 tiles of
+// <= 64 KiB, so packed fields of composed window maps fit; across windows the
+// accumulator is kept unpacked.
+__device__ __forceinline__ void publish_seg(uint64_t *status, uint32_t tile, uint64_t map)
+{
+    if ((threadIdx.x & (kWave - 1)) == 0)
+        granule_store(&status[tile], tile == 0 ? (kFlagP | sm_compose(sm_const(0, 0), map))
+                                               : (kFlagA | map));
+}
+
+__device__ __forceinline__ uint64_t lookback_seg(uint64_t *status, uint32_t tile, uint64_t map,
+                                                 Ctrl *ctrl)
+{
+    const int lane = threadIdx.x & (kWave - 1);
+    const uint64_t kPay = (1ull << 56) - 1;
+    if (tile == 0)
+        return sm_const(0, 0);
+    // accumulator for windows without an inclusive prefix (newest part), unpacked
+    uint32_t acc_kind = 0;  // 0 no-nat, 1 nat
+    uint64_t acc_a = 0, acc_b = 0;
+    uint32_t acc_c = 0;
+    int64_t j = (int64_t)tile - 1;
+    uint32_t spins = 0;
+    for (;;) {
+        const int64_t idx = j - lane;
+        uint64_t s;
+        for (;;) {
+            s = idx >= 0 ? granule_load(&status[idx]) : (kFlagP | sm_const(0, 0));
+            if (window_ready(s))
+                break;
+            if (++spins > kSpinLimit) {
+                if (lane == 0)
+                    raise_error(ctrl, FLRL_E_TIMEOUT);
+                return sm_const(0, 0);
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        const unsigned long long pm = __ballot((s >> 62) == 2);
+        const int first = pm ? __ffsll(pm) - 1 : kWave;
+        uint64_t m = lane < first ? (s & kPay) : (lane == first ? sm_const(sm_h(s), sm_c(s)) : 0ull);
+        // suffix composition: lane l ends with compose(m_63 .. m_l); identity = no-nat L 0
+#pragma unroll
+        for (int o = 1; o < kWave; o <<= 1) {
+            const uint64_t older = __shfl_down(m, o, kWave);
+            if (lane + o < kWave)
+                m = sm_compose(older, m);
+        }
+        const uint64_t win = __shfl(m, 0, kWave);  // oldest-first composition of the window
+        // combine with the newer accumulator: win then acc
+        uint64_t res;
+        if ((win & kSmKind) == kSmConst) {
+            uint64_t H = sm_h(win);
+            uint32_t c = sm_c(win);
+            if (acc_kind == 1) {
+                H += splits64(c, acc_a) + acc_b;
+                c = acc_c;
+            } else {
+                H += splits64(c, acc_a);
+                c = add_c64(c, acc_a);
+            }
+            res = sm_const(H, c);
+            if (lane == 0)
+                granule_store(&status[tile], kFlagP | sm_compose(res, map));
+            return res;
+        }
+        // no inclusive prefix in this window: fold it into the accumulator
+        if ((win & kSmKind) == kSmNat) {
+            if (acc_kind == 1) {
+                acc_b = sm_b(win) + splits64(sm_c(win), acc_a) + acc_b;
+                acc_a = sm_a(win);
+            } else {
+                acc_b = sm_b(win) + splits64(sm_c(win), acc_a);
+                acc_c = add_c64(sm_c(win), acc_a);
+                acc_a = sm_a(win);
+                acc_kind = 1;
+            }
+        } else {
+            acc_a = sm_a(win) + acc_a;
+        }
+        j -= kWave;
+    }
+}
+
+// Heads of one lane-item given the chunk state c0 before its first byte: the
+// natural heads, plus at most one split head where the state first wraps to 0
+// (offset j0 = (255 - c0) mod 255), if no natural head comes at or before it.
+// After any head the state restarts at 1, so a second split needs 255 more bytes.
+__device__ __forceinline__ uint32_t lane_heads(uint32_t nat, uint32_t c0, uint32_t vb)
+{
+    const uint32_t j0 = c0 == 0 ? 0u : 255u - c0;
+    const uint32_t below = (1u << (j0 & 15)) - 1u;
+    const bool split = j0 < vb && (nat & below) == 0;
+    return nat | (split ? 1u << (j0 & 15) : 0u);
+}
+
+// Block-wide (T threads) exclusive sum; returns the exclusive prefix of v and
+// the total in *total. Uses s_w[T/64]; two barriers.
+template <int T>
+__device__ __forceinline__ uint32_t block_excl_sum(uint32_t v, uint32_t *s_w, uint32_t *total)
+{
+    const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
+    const uint32_t inc = wave_incl_scan_u32(v);
+    if (lane == kWave - 1)
+        s_w[w] = inc;
+    __syncthreads();
+    uint32_t before = 0, tot = 0;
+#pragma unroll
+    for (int i = 0; i < T / kWave; ++i) {
+        before += i < w ? s_w[i] : 0u;
+        tot += s_w[i];
+    }
+    __syncthreads();
+    *total = tot;
+    return before + inc - v;
+}
+
+// Copy cnt staged bytes from LDS to global memory (the workgroup's threads).
+template <int T>
+__device__ __forceinline__ void copy_out(uint8_t *__restrict__ dst, const uint8_t *src, uint32_t cnt)
+{
+    for (uint32_t j = threadIdx.x; j < cnt; j += T)
+        dst[j] = src[j];
+}
+
+// Emission of run (count, value) records for the heads of one lane-item, into
+// slots starting at `slot`: head at byte i ends the run before it, whose count
+// is the chunk state before i (c0 + i for the lane's first head, the distance
+// to the previous head after it; 255 for a full chunk) and value is byte i-1.
+__device__ __forceinline__ void emit_lane(uint32_t h, uint32_t c0, const u32x4 &x, uint32_t pbyte,
+                                          uint8_t *stc, uint8_t *stv, uint32_t slot)
+{
+    uint32_t prev_i = 0;
+    bool seen = false;
+    while (h) {
+        const uint32_t i = __ffs(h) - 1;
+        h &= h - 1;
+        uint32_t cb = seen ? i - prev_i : c0 + i;
+        cb = cb >= 255u ? cb - 255u : cb;
+        seen = true;
+        prev_i = i;
+        stc[slot] = (uint8_t)(cb == 0 ? 255u : cb);
+        stv[slot] = (uint8_t)(i == 0 ? pbyte : byte_at(x, i - 1));
+        ++slot;
+    }
+}
+
+// One tile of TB bytes per workgroup (ticket order). Heads from the tile's first
+// natural head on do not depend on the incoming state, so their runs are staged
+// in LDS in tile order before the look-back (the register copy of the tile dies
+// there); after it, the c_in-dependent prefix (split heads before the first
+// natural head, and the count of the run that head ends) is written directly
+// and the staged records leave in contiguous stores. A tile with more than CAP
+// such heads (incompressible data) re-reads its bytes and emits per item.
+template <int T, int ITEMS, int CAP>
 __global__ __launch_bounds__(T) void rl_encode_kernel(
     const uint8_t *__restrict__ in, uint64_t n, uint32_t ntiles, uint8_t *__restrict__ counts,
-    uint8_t *__restrict__ values, uint64_t *__restrict__ runs_out, Ctrl *ctrl,
-    uint64_t *st_phase, uint64_t *st_heads)
+    uint8_t *__restrict__ values, uint64_t *__restrict__ runs_out, Ctrl *ctrl, uint64_t *status)
 {
     constexpr int W = T / kWave;
     constexpr int WB = kWave * 16 * ITEMS;
     constexpr int TB = WB * W;
+    static_assert(CAP >= W * kWave * 16, "overflow path stages one wave-item per wave");
     __shared__ uint32_t s_wmap[W];
-    __shared__ uint32_t s_whead[W];
-    __shared__ uint8_t s_stc[W][kWave * 16];
-    __shared__ uint8_t s_stv[W][kWave * 16];
-    __shared__ uint32_t s_ticket, s_cin;
-    __shared__ uint64_t s_hin;
+    __shared__ uint32_t s_wfirst[W];
+    __shared__ uint32_t s_wh[W];
+    __shared__ uint8_t s_stc[CAP];
+    __shared__ uint8_t s_stv[CAP];
+    __shared__ uint32_t s_ticket;
+    __shared__ uint64_t s_state;
 
     const int tid = threadIdx.x;
     const int lane = tid & (kWave - 1);
     const int w = tid / kWave;
+    FLRL_RL_PHASE_BEGIN();
     const uint32_t tile = take_ticket(ctrl, &s_ticket);
     const uint64_t tile_off = (uint64_t)tile * TB;
     const uint64_t wave_off = tile_off + (uint64_t)w * WB;
+    FLRL_RL_PHASE(0);
 
     // ---- load this wave's contiguous 16 KiB (lane: chunk k*64 + lane) -----
     u32x4 a[ITEMS];
@@ -198,9 +364,12 @@ __global__ __launch_bounds__(T) void rl_encode_kernel(
     }
     const uint32_t pwave = (wave_off > 0 && wave_off <= n) ? in[wave_off - 1] : 0u;
 
-    // ---- natural heads and the lane -> wave exclusive scan of phase maps --
-    uint32_t nat[ITEMS], rel[ITEMS], prevb[ITEMS];
+    // ---- natural heads; lane -> wave exclusive scan of phase maps -----------
+    // st[k] = nat (16 bits) | rel map (9 bits) << 16 | valid bytes (5 bits) << 25;
+    // pb = previous bytes, 4 per word
+    uint32_t st[ITEMS], pb[ITEMS / 4];
     uint32_t carry = kMapIdent;
+    uint32_t first_nat = 0xFFFFFFFFu;  // wave-local byte offset of the first natural head
 #pragma unroll
     for (int k = 0; k < ITEMS; ++k) {
         const uint32_t up = __shfl_up(a[k].w, 1, kWave) >> 24;
@@ -208,137 +377,191 @@ __global__ __launch_bounds__(T) void rl_encode_kernel(
             k > 0 ? (uint32_t)__builtin_amdgcn_readlane((int)a[k > 0 ? k - 1 : 0].w, kWave - 1) >> 24
                   : pwave;
         const uint32_t p = lane > 0 ? up : last_prev_item;
-        prevb[k] = p;
+        if ((k & 3) == 0)
+            pb[k / 4] = 0;
+        pb[k / 4] |= p << (8 * (k & 3));
         const uint64_t gpos = wave_off + (uint64_t)(k * kWave + lane) * 16;
         const uint32_t vb = gpos >= n ? 0u : (n - gpos >= 16 ? 16u : (uint32_t)(n - gpos));
         uint32_t m = nat_mask(a[k], p);
         if (gpos == 0)
             m |= 1u;
         m &= vb >= 16 ? 0xFFFFu : ((1u << vb) - 1u);
-        nat[k] = m;
         const uint32_t lmap = m ? pm_make(true, vb - (31u - __clz(m))) : pm_make(false, vb);
         const uint32_t incl = wave_incl_scan_map(lmap);
         const uint32_t excl = __shfl_up(incl, 1, kWave);
-        rel[k] = pm_compose(carry, lane > 0 ? excl : kMapIdent);
+        st[k] = m | (pm_compose(carry, lane > 0 ? excl : kMapIdent) << 16) | (vb << 25);
         carry = pm_compose(carry, (uint32_t)__builtin_amdgcn_readlane((int)incl, kWave - 1));
+        const unsigned long long has = __ballot(m != 0);
+        if (first_nat == 0xFFFFFFFFu && has) {
+            const int l = __ffsll(has) - 1;
+            const uint32_t ml = (uint32_t)__shfl(m, l, kWave);
+            first_nat = (uint32_t)((k * kWave + l) * 16 + (__ffs(ml) - 1));
+        }
     }
-    if (lane == 0)
+    FLRL_RL_PHASE(1);
+    if (lane == 0) {
         s_wmap[w] = carry;
+        s_wfirst[w] = first_nat;
+    }
     __syncthreads();
-    uint32_t tile_map = kMapIdent, wave_pre = kMapIdent;
+    uint32_t tile_map = kMapIdent, wave_pre = kMapIdent, tile_first = 0xFFFFFFFFu;
 #pragma unroll
     for (int v = 0; v < W; ++v) {
         if (v == w)
             wave_pre = tile_map;
         tile_map = pm_compose(tile_map, s_wmap[v]);
+        if (tile_first == 0xFFFFFFFFu && s_wfirst[v] != 0xFFFFFFFFu)
+            tile_first = (uint32_t)(v * WB) + s_wfirst[v];
     }
+    const uint32_t tile_len = (uint32_t)(n - tile_off < (uint64_t)TB ? n - tile_off : TB);
 
-    // ---- look-back 1: chunk state at the tile start ----------------------
-    if (w == 0) {
-        if (lane == 0 && tile > 0)
-            granule_store(&st_phase[tile], kFlagA | tile_map);
-        const uint32_t c = lookback_phase(st_phase, tile, tile_map, ctrl);
-        if (lane == 0)
-            s_cin = c;
-    }
-    __syncthreads();
-    const uint32_t c_wave = pm_apply(wave_pre, s_cin);
-
-    // ---- heads (natural, or chunk full) and their counts per lane-item ----
-    uint32_t head[ITEMS], cst[ITEMS];
-    uint32_t wheads = 0;
+    // ---- state-independent heads: the natural heads up to the lane holding the
+    // first one, then every head (lane states there are constants of the scan;
+    // any stand-in incoming state, here 1, gives them)
+    const uint32_t cw = pm_apply(wave_pre, 1);
+    uint32_t hc = 0;
 #pragma unroll
     for (int k = 0; k < ITEMS; ++k) {
-        const uint32_t c0 = pm_apply(rel[k], c_wave);
-        cst[k] = c0;
-        uint32_t h = nat[k];
-        if (c0 == 0 || c0 >= 240) {  // a split can only fall inside this lane then
-            const uint64_t gpos = wave_off + (uint64_t)(k * kWave + lane) * 16;
-            const uint32_t vb = gpos >= n ? 0u : (n - gpos >= 16 ? 16u : (uint32_t)(n - gpos));
-            uint32_t c = c0;
-            h = 0;
-            for (uint32_t i = 0; i < vb; ++i) {
-                if (((nat[k] >> i) & 1u) || c == 0) {
-                    h |= 1u << i;
-                    c = 1;
-                } else {
-                    c = c + 1 == 255u ? 0u : c + 1;
-                }
-            }
-        }
-        head[k] = h;
-        wheads += __popc(h);
+        const uint32_t off = (uint32_t)(w * WB + (k * kWave + lane) * 16);
+        const uint32_t nat = st[k] & 0xFFFFu;
+        hc += __popc(off <= tile_first ? nat
+                                       : lane_heads(nat, pm_apply((st[k] >> 16) & 0x1FFu, cw), st[k] >> 25));
     }
-    wheads = (uint32_t)wave_sum_u64(wheads);
-    if (lane == 0)
-        s_whead[w] = wheads;
+    {
+        const uint32_t wsum = (uint32_t)wave_sum_u64(hc);
+        if (lane == 0)
+            s_wh[w] = wsum;
+    }
     __syncthreads();
-    uint32_t tile_heads = 0, wave_hpre = 0;
+    uint32_t K = 0, wave_base = 0;
 #pragma unroll
     for (int v = 0; v < W; ++v) {
-        wave_hpre += v < w ? s_whead[v] : 0u;
-        tile_heads += s_whead[v];
+        wave_base += v < w ? s_wh[v] : 0u;
+        K += s_wh[v];
     }
+    const uint32_t pre = K ? tile_first : tile_len;
+    if (w == 0)
+        publish_seg(status, tile, K ? sm_nat(tile_first, K, tile_map & 0xFFu) : sm_nonat(tile_len));
+    FLRL_RL_PHASE(2);
 
-    // ---- look-back 2: index of the tile's first head -----------------------
+    // ---- stage the state-independent runs in tile order ---------------------
+    const bool staged = K <= (uint32_t)CAP;
+    if (staged) {
+        // recompute the heads rather than keep the pass above's (registers)
+#pragma unroll
+        for (int k = 0; k < ITEMS; ++k)
+            asm volatile("" : "+v"(st[k]));
+        uint32_t base = wave_base;
+#pragma unroll
+        for (int k = 0; k < ITEMS; ++k) {
+            const uint32_t off = (uint32_t)(w * WB + (k * kWave + lane) * 16);
+            const uint32_t nat = st[k] & 0xFFFFu;
+            const uint32_t c0 = pm_apply((st[k] >> 16) & 0x1FFu, cw);
+            const uint32_t h = off <= tile_first ? nat : lane_heads(nat, c0, st[k] >> 25);
+            const uint32_t cnt = __popc(h);
+            const uint32_t inc = wave_incl_scan_u32(cnt);
+            if (h)
+                emit_lane(h, c0, a[k], (pb[k / 4] >> (8 * (k & 3))) & 0xFFu, s_stc, s_stv,
+                          base + inc - cnt);
+            base += (uint32_t)__builtin_amdgcn_readlane((int)inc, kWave - 1);
+        }
+    }
+    FLRL_RL_PHASE(3);
+
+    // ---- one look-back: (heads before the tile, chunk state at its start) --
     if (w == 0) {
-        const uint64_t e = lookback_sum(st_heads, tile, tile_heads, ctrl);
+        const uint64_t state = lookback_seg(status, tile, K ? sm_nat(tile_first, K, tile_map & 0xFFu)
+                                                             : sm_nonat(tile_len), ctrl);
         if (lane == 0)
-            s_hin = e;
+            s_state = state;
     }
     __syncthreads();
-    const uint64_t h_in = s_hin;
+    FLRL_RL_PHASE(4);
+    const uint64_t h_in = sm_h(s_state);
+    const uint32_t c_in = sm_c(s_state);
+    const uint32_t S = splits(c_in, pre);  // split heads before the first natural head
+    const uint64_t g0 = h_in + S;          // global index of the first natural head
 
-    // ---- emit: head g writes run g-1 (count = chunk state before it, value =
-    // the byte before it), staged per wave-item in LDS, then stored as bytes
-    uint64_t g_item = h_in + wave_hpre;  // global index of the item's first head
-    uint8_t *stc = s_stc[w];
-    uint8_t *stv = s_stv[w];
-#pragma unroll
-    for (int k = 0; k < ITEMS; ++k) {
-        const uint32_t h = head[k];
-        const uint32_t cnt = __popc(h);
-        const uint32_t inc = wave_incl_scan_u32(cnt);
-        const uint32_t item_total = (uint32_t)__builtin_amdgcn_readlane((int)inc, kWave - 1);
-        if (h) {
-            uint32_t slot = inc - cnt;
-            // chunk state before the first head at byte i: no head in between,
-            // so c0 just advanced i bytes; before a later head: distance (< 16)
-            uint32_t prev_i = 0;
-            bool seen = false;
-            uint32_t hm = h;
-            while (hm) {
-                const uint32_t i = __ffs(hm) - 1;
-                hm &= hm - 1;
-                uint32_t cb = seen ? i - prev_i : cst[k] + i;
-                cb = cb >= 255u ? cb - 255u : cb;
-                seen = true;
-                prev_i = i;
-                stc[slot] = (uint8_t)(cb == 0 ? 255u : cb);
-                stv[slot] = (uint8_t)(i == 0 ? prevb[k] : byte_at(a[k], i - 1));
-                ++slot;
+    // split heads H_in+s end full 255-byte chunks of the byte the tile starts with
+    if (S) {
+        const uint8_t v0 = in[tile_off];
+        for (uint32_t s2 = tid; s2 < S; s2 += T) {
+            const uint64_t g = h_in + s2;
+            if (g > 0) {
+                counts[g - 1] = 255;
+                values[g - 1] = v0;
             }
         }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        for (uint32_t j = lane; j < item_total; j += kWave) {
-            const uint64_t gi = g_item + j;
-            if (gi > 0) {
-                counts[gi - 1] = stc[j];
-                values[gi - 1] = stv[j];
-            }
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        g_item += item_total;
     }
+    if (staged) {
+        if (K) {
+            if (tid == 0 && g0 > 0) {
+                const uint32_t c = add_c(c_in, pre);
+                counts[g0 - 1] = (uint8_t)(c == 0 ? 255u : c);
+                values[g0 - 1] = s_stv[0];
+            }
+            copy_out<T>(counts + g0, s_stc + 1, K - 1);
+            copy_out<T>(values + g0, s_stv + 1, K - 1);
+        }
+    } else {
+        // incompressible tile: re-read the bytes and emit per wave-item with the
+        // true states (one wave-item's records staged per wave in LDS)
+        const uint32_t c_wave = pm_apply(wave_pre, c_in);
+        uint32_t th = 0;
+#pragma unroll
+        for (int k = 0; k < ITEMS; ++k)
+            th += __popc(lane_heads(st[k] & 0xFFFFu, pm_apply((st[k] >> 16) & 0x1FFu, c_wave), st[k] >> 25));
+        {
+            const uint32_t wsum = (uint32_t)wave_sum_u64(th);
+            __syncthreads();
+            if (lane == 0)
+                s_wh[w] = wsum;
+            __syncthreads();
+        }
+        uint64_t g_item = h_in;
+        for (int v = 0; v < w; ++v)
+            g_item += s_wh[v];
+        uint8_t *stc = s_stc + w * (CAP / W);
+        uint8_t *stv = s_stv + w * (CAP / W);
+#pragma unroll 1
+        for (int k = 0; k < ITEMS; ++k) {
+            const uint64_t gpos = wave_off + (uint64_t)(k * kWave + lane) * 16;
+            const u32x4 x = load16_tail(in, gpos, n);
+            const uint32_t c0 = pm_apply((st[k] >> 16) & 0x1FFu, c_wave);
+            const uint32_t h = lane_heads(st[k] & 0xFFFFu, c0, st[k] >> 25);
+            const uint32_t cnt = __popc(h);
+            const uint32_t inc = wave_incl_scan_u32(cnt);
+            const uint32_t item_total = (uint32_t)__builtin_amdgcn_readlane((int)inc, kWave - 1);
+            uint32_t pbyte = 0;
+#pragma unroll
+            for (int q = 0; q < ITEMS / 4; ++q)
+                pbyte = q == k / 4 ? pb[q] : pbyte;
+            pbyte = (pbyte >> (8 * (k & 3))) & 0xFFu;
+            if (h)
+                emit_lane(h, c0, x, pbyte, stc, stv, inc - cnt);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            for (uint32_t j = lane; j < item_total; j += kWave) {
+                const uint64_t gi = g_item + j;
+                if (gi > 0) {
+                    counts[gi - 1] = stc[j];
+                    values[gi - 1] = stv[j];
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            g_item += item_total;
+        }
+    }
+    FLRL_RL_PHASE(5);
+    FLRL_RL_PHASE_END();
 
     // ---- the final run (ends at byte n-1) ----------------------------------
     if (tile + 1 == ntiles && tid == 0) {
-        const uint64_t R = h_in + tile_heads;
-        const uint32_t c_end = pm_apply(tile_map, s_cin);
+        const uint64_t R = g0 + K;
+        const uint32_t c_end = pm_apply(tile_map, c_in);
         counts[R - 1] = (uint8_t)(c_end == 0 ? 255u : c_end);
         values[R - 1] = in[n - 1];
         *runs_out = R;
@@ -530,7 +753,7 @@ struct RlEncLayout {
     explicit RlEncLayout(size_t n)
     {
         tiles = div_up(n, (size_t)kRlTileBytes);
-        bytes = sizeof(Ctrl) + 2 * round_up(tiles * 8, 16);
+        bytes = sizeof(Ctrl) + round_up(tiles * 8, 16);
     }
 };
 
@@ -577,11 +800,10 @@ extern "C" int flrl_rl_encode_device(const uint8_t *d_in, size_t n, uint8_t *d_c
     if (L.tiles > 0xFFFFFFFFull)
         return set_error(FLRL_E_ARG, "flrl_rl_encode_device: input too large");
     Ctrl *ctrl = static_cast<Ctrl *>(d_scratch);
-    uint64_t *st_phase = reinterpret_cast<uint64_t *>(ctrl + 1);
-    uint64_t *st_heads = st_phase + round_up(L.tiles * 8, 16) / 8;
-    hipLaunchKernelGGL((rl_encode_kernel<kRlThreads, kRlItems>), dim3((uint32_t)L.tiles),
+    uint64_t *status = reinterpret_cast<uint64_t *>(ctrl + 1);
+    hipLaunchKernelGGL((rl_encode_kernel<kRlThreads, kRlItems, kRlStage>), dim3((uint32_t)L.tiles),
                        dim3(kRlThreads), 0, s, d_in, (uint64_t)n, (uint32_t)L.tiles, d_counts,
-                       d_values, d_runs, ctrl, st_phase, st_heads);
+                       d_values, d_runs, ctrl, status);
     FLRL_HIP(hipGetLastError());
     return FLRL_OK;
 }

@@ -1,0 +1,119 @@
+// ubench_rl.hip — timing + per-phase cycle breakdown of the library's RL encode
+// (the product kernel itself, compiled in with its phase hooks enabled).
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 [-DSTAMP] -I include \
+//         -I fl-rl-compression-mpi_amd/csrc scripts/ubench_rl.hip -o scripts/ubench_rl.bin
+//   scripts/ubench_rl.bin [kind=2(runs32)] [n=1 GiB] [reps=20]
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+
+__device__ unsigned long long g_ph[64];
+__device__ __forceinline__ uint64_t rl_stamp()
+{
+    uint64_t t;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    return t;
+}
+#ifdef STAMP
+#define FLRL_RL_PHASE_BEGIN() uint64_t _t0 = rl_stamp(), _t1 = 0, _ph[6] = {0, 0, 0, 0, 0, 0}
+#define FLRL_RL_PHASE(k)                                                                   \
+    do {                                                                                   \
+        __builtin_amdgcn_sched_barrier(0);                                                 \
+        _t1 = rl_stamp();                                                                  \
+        _ph[k] += _t1 - _t0;                                                               \
+        _t0 = _t1;                                                                         \
+        __builtin_amdgcn_sched_barrier(0);                                                 \
+    } while (0)
+#define FLRL_RL_PHASE_END()                                                                \
+    do {                                                                                   \
+        if ((threadIdx.x & 63) == 0)                                                       \
+            for (int _i = 0; _i < 6; ++_i)                                                 \
+                atomicAdd(&g_ph[(threadIdx.x / 64) * 8 + _i], (unsigned long long)_ph[_i]); \
+    } while (0)
+#else
+#define FLRL_RL_PHASE_BEGIN() ((void)0)
+#define FLRL_RL_PHASE(k) ((void)0)
+#define FLRL_RL_PHASE_END() ((void)0)
+#endif
+
+#include "flrl_common.hip"
+#include "flrl_rl.hip"
+
+#define CK(x)                                                                  \
+    do {                                                                       \
+        hipError_t e_ = (x);                                                   \
+        if (e_ != hipSuccess) {                                                \
+            fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
+            exit(1);                                                           \
+        }                                                                      \
+    } while (0)
+
+int main(int argc, char **argv)
+{
+    const int kind = argc > 1 ? atoi(argv[1]) : 3;  // 3 = runs32
+    const size_t n = argc > 2 ? strtoull(argv[2], nullptr, 0) : (1ull << 30);
+    const int reps = argc > 3 ? atoi(argv[3]) : 20;
+    uint8_t *d_in, *d_c, *d_v;
+    uint64_t *d_runs;
+    void *d_scr;
+    const size_t scr = flrl_rl_scratch_bytes(n);
+    CK(hipMalloc(&d_in, n + 64));
+    CK(hipMalloc(&d_c, n + 64));
+    CK(hipMalloc(&d_v, n + 64));
+    CK(hipMalloc(&d_runs, 8));
+    CK(hipMalloc(&d_scr, scr));
+    {
+        uint8_t *h = (uint8_t *)malloc(n);
+        if (flrl_gen_host(kind, 42, 0, h, n) != FLRL_OK) {
+            fprintf(stderr, "gen: %s\n", flrl_last_error());
+            return 1;
+        }
+        CK(hipMemcpy(d_in, h, n, hipMemcpyHostToDevice));
+        free(h);
+    }
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    float best = 1e30f, sum = 0;
+    for (int r = 0; r < reps + 3; ++r) {
+        if (r == 3) {
+            unsigned long long z[64] = {};
+            CK(hipMemcpyToSymbol(HIP_SYMBOL(g_ph), z, sizeof(z)));
+        }
+        CK(hipEventRecord(e0, nullptr));
+        if (flrl_rl_encode_device(d_in, n, d_c, d_v, d_runs, d_scr, scr, nullptr) != FLRL_OK) {
+            fprintf(stderr, "encode: %s\n", flrl_last_error());
+            return 1;
+        }
+        CK(hipEventRecord(e1, nullptr));
+        CK(hipEventSynchronize(e1));
+        float ms;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        if (r >= 3) {
+            sum += ms;
+            best = ms < best ? ms : best;
+        }
+    }
+    uint64_t runs = 0;
+    CK(hipMemcpy(&runs, d_runs, 8, hipMemcpyDeviceToHost));
+    printf("rl_encode kind %d n %zu runs %llu: avg %.4f ms best %.4f ms (%.1f GB/s alg avg)  err %d\n", kind, n,
+           (unsigned long long)runs, sum / reps, best, (n + 2.0 * runs) / (sum / reps) / 1e6,
+           flrl_scratch_error(d_scr, nullptr));
+#ifdef STAMP
+    unsigned long long ph[64];
+    CK(hipMemcpyFromSymbol(ph, HIP_SYMBOL(g_ph), sizeof(ph)));
+    const char *names[6] = {"ticket", "load+nat+mapscan", "wavecombine+fake+sum", "lookback+barrier",
+                            "true heads+sum", "emit"};
+    for (int w = 0; w < 4; ++w) {
+        unsigned long long tot = 0;
+        for (int i = 0; i < 6; ++i)
+            tot += ph[w * 8 + i];
+        printf("wave %d:", w);
+        for (int i = 0; i < 6; ++i)
+            printf("  %s %.1f%%", names[i], 100.0 * ph[w * 8 + i] / (tot ? tot : 1));
+        printf("\n");
+    }
+#endif
+    return 0;
+}
