@@ -44,11 +44,10 @@
 
 namespace flrl {
 
-constexpr int kRlThreads = 256;                      // encode workgroup: 4 waves
-constexpr int kRlItems = 16;                         // 16 x 16 B per lane
-constexpr int kRlWaveBytes = kWave * 16 * kRlItems;  // 16 KiB per wave (contiguous)
-constexpr int kRlTileBytes = kRlWaveBytes * (kRlThreads / kWave);  // 64 KiB
-constexpr int kRlStage = 16384;  // runs per tile staged in LDS (2 x 16 KiB)
+constexpr int kRlThreads = 512;                     // encode workgroup: 8 waves
+constexpr int kRlLaneBytes = 128;                   // contiguous bytes per lane
+constexpr int kRlTileBytes = kRlLaneBytes * kRlThreads;  // 64 KiB, held in LDS
+constexpr int kRlDenseRun = 32;  // > this many heads per lane (mean run < 4 B): row-wise emission
 
 constexpr int kRdRuns = 4096;        // runs per decode tile
 constexpr int kRdThreads = 256;
@@ -287,57 +286,26 @@ __device__ __forceinline__ uint32_t block_excl_sum(uint32_t v, uint32_t *s_w, ui
     return before + inc - v;
 }
 
-// Copy cnt staged bytes from LDS to global memory (the workgroup's threads).
-template <int T>
-__device__ __forceinline__ void copy_out(uint8_t *__restrict__ dst, const uint8_t *src, uint32_t cnt)
-{
-    for (uint32_t j = threadIdx.x; j < cnt; j += T)
-        dst[j] = src[j];
-}
-
-// Emission of run (count, value) records for the heads of one lane-item, into
-// slots starting at `slot`: head at byte i ends the run before it, whose count
-// is the chunk state before i (c0 + i for the lane's first head, the distance
-// to the previous head after it; 255 for a full chunk) and value is byte i-1.
-__device__ __forceinline__ void emit_lane(uint32_t h, uint32_t c0, const u32x4 &x, uint32_t pbyte,
-                                          uint8_t *stc, uint8_t *stv, uint32_t slot)
-{
-    uint32_t prev_i = 0;
-    bool seen = false;
-    while (h) {
-        const uint32_t i = __ffs(h) - 1;
-        h &= h - 1;
-        uint32_t cb = seen ? i - prev_i : c0 + i;
-        cb = cb >= 255u ? cb - 255u : cb;
-        seen = true;
-        prev_i = i;
-        stc[slot] = (uint8_t)(cb == 0 ? 255u : cb);
-        stv[slot] = (uint8_t)(i == 0 ? pbyte : byte_at(x, i - 1));
-        ++slot;
-    }
-}
-
-// One tile of TB bytes per workgroup (ticket order). Heads from the tile's first
-// natural head on do not depend on the incoming state, so their runs are staged
-// in LDS in tile order before the look-back (the register copy of the tile dies
-// there); after it, the c_in-dependent prefix (split heads before the first
-// natural head, and the count of the run that head ends) is written directly
-// and the staged records leave in contiguous stores. A tile with more than CAP
-// such heads (incompressible data) re-reads its bytes and emits per item.
-template <int T, int ITEMS, int CAP>
+// One tile of T/64 x 64 lanes x LB bytes per workgroup, in ticket order. The
+// tile lands in LDS by LDS-DMA (global_load_lds, 1 KiB per wave-instruction,
+// coalesced), swizzled so that every lane can then read ITS OWN contiguous LB
+// bytes conflict-free: lane row r keeps chunk c at r*LB + ((c ^ (r & 7)) * 16).
+// Each lane folds its bytes into one segment map (so a wave needs ONE scan,
+// not one per chunk), the tile's map goes through the look-back, and every lane
+// then knows (global head index, chunk state) at its first byte and emits its
+// own runs in order, re-reading its bytes from LDS.
+template <int T, int LB>
 __global__ __launch_bounds__(T) void rl_encode_kernel(
     const uint8_t *__restrict__ in, uint64_t n, uint32_t ntiles, uint8_t *__restrict__ counts,
     uint8_t *__restrict__ values, uint64_t *__restrict__ runs_out, Ctrl *ctrl, uint64_t *status)
 {
     constexpr int W = T / kWave;
-    constexpr int WB = kWave * 16 * ITEMS;
+    constexpr int CH = LB / 16;  // 16-byte chunks per lane
+    constexpr int WB = kWave * LB;
     constexpr int TB = WB * W;
-    static_assert(CAP >= W * kWave * 16, "overflow path stages one wave-item per wave");
-    __shared__ uint32_t s_wmap[W];
-    __shared__ uint32_t s_wfirst[W];
-    __shared__ uint32_t s_wh[W];
-    __shared__ uint8_t s_stc[CAP];
-    __shared__ uint8_t s_stv[CAP];
+    static_assert(LB == 128, "the swizzle and the 2 x u64 head masks assume 8 chunks per lane");
+    __shared__ __attribute__((aligned(16))) uint8_t s_data[TB];
+    __shared__ uint64_t s_wmap[W];
     __shared__ uint32_t s_ticket;
     __shared__ uint64_t s_state;
 
@@ -348,220 +316,214 @@ __global__ __launch_bounds__(T) void rl_encode_kernel(
     const uint32_t tile = take_ticket(ctrl, &s_ticket);
     const uint64_t tile_off = (uint64_t)tile * TB;
     const uint64_t wave_off = tile_off + (uint64_t)w * WB;
-    FLRL_RL_PHASE(0);
 
-    // ---- load this wave's contiguous 16 KiB (lane: chunk k*64 + lane) -----
-    u32x4 a[ITEMS];
-    if (wave_off + WB <= n) {
-        const u32x4 *src = reinterpret_cast<const u32x4 *>(in + wave_off);
+    // ---- tile -> LDS. Instruction j of wave w fills rows w*64 + j*8 .. +7;
+    // lane writes row j*8 + lane/8 at column lane&7, i.e. chunk (lane&7)^(row&7)
+    {
+        const uint32_t col = (uint32_t)lane & 7u;
+        const uint32_t c = col ^ (((uint32_t)lane >> 3) & 7u);
+        uint8_t *dst = s_data + w * WB;
+        if (wave_off + WB <= n) {
 #pragma unroll
-        for (int k = 0; k < ITEMS; ++k)
-            a[k] = __builtin_nontemporal_load(src + k * kWave + lane);
-    } else {
+            for (int j = 0; j < WB / 1024; ++j) {
+                const uint8_t *src = in + wave_off + (uint32_t)(j * 8 + lane / 8) * LB + c * 16;
+                __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)src,
+                                                 (__attribute__((address_space(3))) void *)(dst + j * 1024),
+                                                 16, 0, 0);
+            }
+        } else {
 #pragma unroll
-        for (int k = 0; k < ITEMS; ++k)
-            a[k] = load16_tail(in, wave_off + (uint64_t)(k * kWave + lane) * 16, n);
-    }
-    const uint32_t pwave = (wave_off > 0 && wave_off <= n) ? in[wave_off - 1] : 0u;
-
-    // ---- natural heads; lane -> wave exclusive scan of phase maps -----------
-    // st[k] = nat (16 bits) | rel map (9 bits) << 16 | valid bytes (5 bits) << 25;
-    // pb = previous bytes, 4 per word
-    uint32_t st[ITEMS], pb[ITEMS / 4];
-    uint32_t carry = kMapIdent;
-    uint32_t first_nat = 0xFFFFFFFFu;  // wave-local byte offset of the first natural head
-#pragma unroll
-    for (int k = 0; k < ITEMS; ++k) {
-        const uint32_t up = __shfl_up(a[k].w, 1, kWave) >> 24;
-        const uint32_t last_prev_item =
-            k > 0 ? (uint32_t)__builtin_amdgcn_readlane((int)a[k > 0 ? k - 1 : 0].w, kWave - 1) >> 24
-                  : pwave;
-        const uint32_t p = lane > 0 ? up : last_prev_item;
-        if ((k & 3) == 0)
-            pb[k / 4] = 0;
-        pb[k / 4] |= p << (8 * (k & 3));
-        const uint64_t gpos = wave_off + (uint64_t)(k * kWave + lane) * 16;
-        const uint32_t vb = gpos >= n ? 0u : (n - gpos >= 16 ? 16u : (uint32_t)(n - gpos));
-        uint32_t m = nat_mask(a[k], p);
-        if (gpos == 0)
-            m |= 1u;
-        m &= vb >= 16 ? 0xFFFFu : ((1u << vb) - 1u);
-        const uint32_t lmap = m ? pm_make(true, vb - (31u - __clz(m))) : pm_make(false, vb);
-        const uint32_t incl = wave_incl_scan_map(lmap);
-        const uint32_t excl = __shfl_up(incl, 1, kWave);
-        st[k] = m | (pm_compose(carry, lane > 0 ? excl : kMapIdent) << 16) | (vb << 25);
-        carry = pm_compose(carry, (uint32_t)__builtin_amdgcn_readlane((int)incl, kWave - 1));
-        const unsigned long long has = __ballot(m != 0);
-        if (first_nat == 0xFFFFFFFFu && has) {
-            const int l = __ffsll(has) - 1;
-            const uint32_t ml = (uint32_t)__shfl(m, l, kWave);
-            first_nat = (uint32_t)((k * kWave + l) * 16 + (__ffs(ml) - 1));
+            for (int j = 0; j < WB / 1024; ++j) {
+                const uint64_t g = wave_off + (uint32_t)(j * 8 + lane / 8) * LB + c * 16;
+                *reinterpret_cast<u32x4 *>(dst + j * 1024 + lane * 16) = load16_tail(in, g, n);
+            }
         }
     }
-    FLRL_RL_PHASE(1);
-    if (lane == 0) {
-        s_wmap[w] = carry;
-        s_wfirst[w] = first_nat;
+    const uint32_t row = (uint32_t)tid;  // lane row within the tile
+    const uint64_t lane_off = tile_off + (uint64_t)row * LB;
+    const uint32_t vbl = lane_off >= n ? 0u : (n - lane_off >= LB ? (uint32_t)LB : (uint32_t)(n - lane_off));
+    const uint32_t ptile = (tid == 0 && tile_off > 0) ? in[tile_off - 1] : 0u;
+    __syncthreads();  // waits for the LDS-DMA too
+    FLRL_RL_PHASE(0);
+
+    const uint8_t *my = s_data + row * LB;
+    auto chunk = [&](int c) -> u32x4 {
+        return *reinterpret_cast<const u32x4 *>(my + ((c ^ (row & 7u)) * 16));
+    };
+    const uint32_t p0 = row == 0 ? ptile : s_data[(row - 1) * LB + ((7u ^ ((row - 1) & 7u)) * 16) + 15];
+
+    // ---- pass 1: natural heads and the lane's segment map -----------------
+    uint32_t nat[CH / 2];  // 16-bit masks, two per word
+    bool has = false;
+    uint32_t pre = 0, K = 0, cs = 0;
+    {
+        uint32_t p = p0;
+#pragma unroll
+        for (int c = 0; c < CH; ++c) {
+            const u32x4 x = chunk(c);
+            const uint32_t vb = vbl > 16u * c ? (vbl - 16u * c >= 16 ? 16u : vbl - 16u * c) : 0u;
+            uint32_t m = nat_mask(x, p) & (vb >= 16 ? 0xFFFFu : ((1u << vb) - 1u));
+            if (c == 0 && lane_off == 0)
+                m |= 1u;
+            if (c & 1)
+                nat[c / 2] |= m << 16;
+            else
+                nat[c / 2] = m;
+            p = x.w >> 24;
+            if (!has) {
+                if (m) {
+                    has = true;
+                    pre += __ffs(m) - 1;
+                    K = __popc(m);
+                    cs = vb - (31u - __clz(m));
+                } else {
+                    pre += vb;
+                }
+            } else {
+                const uint32_t h = lane_heads(m, cs, vb);
+                K += __popc(h);
+                cs = h ? vb - (31u - __clz(h)) : add_c(cs, vb);
+            }
+        }
     }
+    const uint64_t lmap = has ? sm_nat(pre, K, cs) : sm_nonat(pre);
+
+    // ---- lane -> wave -> tile scans of segment maps ------------------------
+    uint64_t incl = lmap;
+#pragma unroll
+    for (int o = 1; o < kWave; o <<= 1) {
+        const uint64_t up = __shfl_up(incl, o, kWave);
+        if (lane >= o)
+            incl = sm_compose(up, incl);
+    }
+    uint64_t lane_pre = __shfl_up(incl, 1, kWave);
+    if (lane == 0)
+        lane_pre = sm_nonat(0);
+    if (lane == kWave - 1)
+        s_wmap[w] = incl;
     __syncthreads();
-    uint32_t tile_map = kMapIdent, wave_pre = kMapIdent, tile_first = 0xFFFFFFFFu;
+    uint64_t tile_map = sm_nonat(0), wave_pre = sm_nonat(0);
 #pragma unroll
     for (int v = 0; v < W; ++v) {
         if (v == w)
             wave_pre = tile_map;
-        tile_map = pm_compose(tile_map, s_wmap[v]);
-        if (tile_first == 0xFFFFFFFFu && s_wfirst[v] != 0xFFFFFFFFu)
-            tile_first = (uint32_t)(v * WB) + s_wfirst[v];
+        tile_map = sm_compose(tile_map, s_wmap[v]);
     }
-    const uint32_t tile_len = (uint32_t)(n - tile_off < (uint64_t)TB ? n - tile_off : TB);
-
-    // ---- state-independent heads: the natural heads up to the lane holding the
-    // first one, then every head (lane states there are constants of the scan;
-    // any stand-in incoming state, here 1, gives them)
-    const uint32_t cw = pm_apply(wave_pre, 1);
-    uint32_t hc = 0;
-#pragma unroll
-    for (int k = 0; k < ITEMS; ++k) {
-        const uint32_t off = (uint32_t)(w * WB + (k * kWave + lane) * 16);
-        const uint32_t nat = st[k] & 0xFFFFu;
-        hc += __popc(off <= tile_first ? nat
-                                       : lane_heads(nat, pm_apply((st[k] >> 16) & 0x1FFu, cw), st[k] >> 25));
-    }
-    {
-        const uint32_t wsum = (uint32_t)wave_sum_u64(hc);
-        if (lane == 0)
-            s_wh[w] = wsum;
-    }
-    __syncthreads();
-    uint32_t K = 0, wave_base = 0;
-#pragma unroll
-    for (int v = 0; v < W; ++v) {
-        wave_base += v < w ? s_wh[v] : 0u;
-        K += s_wh[v];
-    }
-    const uint32_t pre = K ? tile_first : tile_len;
     if (w == 0)
-        publish_seg(status, tile, K ? sm_nat(tile_first, K, tile_map & 0xFFu) : sm_nonat(tile_len));
-    FLRL_RL_PHASE(2);
-
-    // ---- stage the state-independent runs in tile order ---------------------
-    const bool staged = K <= (uint32_t)CAP;
-    if (staged) {
-        // recompute the heads rather than keep the pass above's (registers)
-#pragma unroll
-        for (int k = 0; k < ITEMS; ++k)
-            asm volatile("" : "+v"(st[k]));
-        uint32_t base = wave_base;
-#pragma unroll
-        for (int k = 0; k < ITEMS; ++k) {
-            const uint32_t off = (uint32_t)(w * WB + (k * kWave + lane) * 16);
-            const uint32_t nat = st[k] & 0xFFFFu;
-            const uint32_t c0 = pm_apply((st[k] >> 16) & 0x1FFu, cw);
-            const uint32_t h = off <= tile_first ? nat : lane_heads(nat, c0, st[k] >> 25);
-            const uint32_t cnt = __popc(h);
-            const uint32_t inc = wave_incl_scan_u32(cnt);
-            if (h)
-                emit_lane(h, c0, a[k], (pb[k / 4] >> (8 * (k & 3))) & 0xFFu, s_stc, s_stv,
-                          base + inc - cnt);
-            base += (uint32_t)__builtin_amdgcn_readlane((int)inc, kWave - 1);
-        }
-    }
-    FLRL_RL_PHASE(3);
+        publish_seg(status, tile, tile_map);
+    FLRL_RL_PHASE(1);
 
     // ---- one look-back: (heads before the tile, chunk state at its start) --
     if (w == 0) {
-        const uint64_t state = lookback_seg(status, tile, K ? sm_nat(tile_first, K, tile_map & 0xFFu)
-                                                             : sm_nonat(tile_len), ctrl);
+        const uint64_t state = lookback_seg(status, tile, tile_map, ctrl);
         if (lane == 0)
             s_state = state;
     }
     __syncthreads();
-    FLRL_RL_PHASE(4);
-    const uint64_t h_in = sm_h(s_state);
-    const uint32_t c_in = sm_c(s_state);
-    const uint32_t S = splits(c_in, pre);  // split heads before the first natural head
-    const uint64_t g0 = h_in + S;          // global index of the first natural head
+    FLRL_RL_PHASE(2);
+    const uint64_t tile_state = s_state;
+    const uint64_t lane_state = sm_compose(sm_compose(tile_state, wave_pre), lane_pre);
+    uint64_t g = sm_h(lane_state);  // global index of the lane's next head
+    const uint32_t c_lane = sm_c(lane_state);
 
-    // split heads H_in+s end full 255-byte chunks of the byte the tile starts with
-    if (S) {
-        const uint8_t v0 = in[tile_off];
-        for (uint32_t s2 = tid; s2 < S; s2 += T) {
-            const uint64_t g = h_in + s2;
-            if (g > 0) {
-                counts[g - 1] = 255;
-                values[g - 1] = v0;
-            }
+    // ---- heads with the true states, then the lane's runs in order ----------
+    uint64_t hm0 = 0, hm1 = 0;  // head masks of chunks 0-3 / 4-7
+    {
+        uint32_t cst = c_lane;
+#pragma unroll
+        for (int c = 0; c < CH; ++c) {
+            const uint32_t vb = vbl > 16u * c ? (vbl - 16u * c >= 16 ? 16u : vbl - 16u * c) : 0u;
+            const uint32_t m = (nat[c / 2] >> (16 * (c & 1))) & 0xFFFFu;
+            const uint32_t h = lane_heads(m, cst, vb);
+            cst = h ? vb - (31u - __clz(h)) : add_c(cst, vb);
+            if (c < 4)
+                hm0 |= (uint64_t)h << (16 * c);
+            else
+                hm1 |= (uint64_t)h << (16 * (c - 4));
         }
     }
-    if (staged) {
-        if (K) {
-            if (tid == 0 && g0 > 0) {
-                const uint32_t c = add_c(c_in, pre);
-                counts[g0 - 1] = (uint8_t)(c == 0 ? 255u : c);
-                values[g0 - 1] = s_stv[0];
+    // Sparse heads (compressible data): every lane walks its own heads; a
+    // wave-instruction's stores then span a few hundred bytes. Dense heads: the
+    // lanes' ranges are far apart, so the wave emits ONE lane row at a time,
+    // lane t taking byte positions t and 64 + t of the row (ranks by popcount),
+    // which keeps every store instruction contiguous.
+    const uint32_t wave_heads =
+        (uint32_t)wave_sum_u64((uint64_t)(__popcll(hm0) + __popcll(hm1)));
+    if (wave_heads <= (uint32_t)(kRlDenseRun * kWave)) {
+        int prev = -1;  // position of the previous head in this lane
+        while (hm0 | hm1) {
+            int pos;
+            if (hm0) {
+                pos = __builtin_ctzll(hm0);
+                hm0 &= hm0 - 1;
+            } else {
+                pos = 64 + __builtin_ctzll(hm1);
+                hm1 &= hm1 - 1;
             }
-            copy_out<T>(counts + g0, s_stc + 1, K - 1);
-            copy_out<T>(values + g0, s_stv + 1, K - 1);
+            uint32_t cnt = prev < 0 ? add_c(c_lane, (uint32_t)pos) : (uint32_t)(pos - prev);
+            cnt = cnt == 0 ? 255u : cnt;
+            uint32_t val;
+            if (pos == 0) {
+                val = p0;
+            } else {
+                const uint32_t q = (uint32_t)pos - 1;
+                val = my[(((q >> 4) ^ (row & 7u)) * 16) + (q & 15u)];
+            }
+            if (g > 0) {
+                counts[g - 1] = (uint8_t)cnt;
+                values[g - 1] = (uint8_t)val;
+            }
+            ++g;
+            prev = pos;
         }
     } else {
-        // incompressible tile: re-read the bytes and emit per wave-item with the
-        // true states (one wave-item's records staged per wave in LDS)
-        const uint32_t c_wave = pm_apply(wave_pre, c_in);
-        uint32_t th = 0;
-#pragma unroll
-        for (int k = 0; k < ITEMS; ++k)
-            th += __popc(lane_heads(st[k] & 0xFFFFu, pm_apply((st[k] >> 16) & 0x1FFu, c_wave), st[k] >> 25));
-        {
-            const uint32_t wsum = (uint32_t)wave_sum_u64(th);
-            __syncthreads();
-            if (lane == 0)
-                s_wh[w] = wsum;
-            __syncthreads();
-        }
-        uint64_t g_item = h_in;
-        for (int v = 0; v < w; ++v)
-            g_item += s_wh[v];
-        uint8_t *stc = s_stc + w * (CAP / W);
-        uint8_t *stv = s_stv + w * (CAP / W);
+        const uint64_t below = ((uint64_t)1 << lane) - 1;
 #pragma unroll 1
-        for (int k = 0; k < ITEMS; ++k) {
-            const uint64_t gpos = wave_off + (uint64_t)(k * kWave + lane) * 16;
-            const u32x4 x = load16_tail(in, gpos, n);
-            const uint32_t c0 = pm_apply((st[k] >> 16) & 0x1FFu, c_wave);
-            const uint32_t h = lane_heads(st[k] & 0xFFFFu, c0, st[k] >> 25);
-            const uint32_t cnt = __popc(h);
-            const uint32_t inc = wave_incl_scan_u32(cnt);
-            const uint32_t item_total = (uint32_t)__builtin_amdgcn_readlane((int)inc, kWave - 1);
-            uint32_t pbyte = 0;
+        for (int r = 0; r < kWave; ++r) {
+            const uint64_t h0 = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(hm0 >> 32), r) << 32) |
+                                (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)hm0, r);
+            const uint64_t h1 = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(hm1 >> 32), r) << 32) |
+                                (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)hm1, r);
+            const uint64_t g_row = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(g >> 32), r) << 32) |
+                                   (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)g, r);
+            const uint32_t c_row = (uint32_t)__builtin_amdgcn_readlane((int)c_lane, r);
+            const uint32_t p_row = (uint32_t)__builtin_amdgcn_readlane((int)p0, r);
+            const uint32_t rr = (uint32_t)(w * kWave + r);
+            const uint8_t *rowp = s_data + rr * LB;
 #pragma unroll
-            for (int q = 0; q < ITEMS / 4; ++q)
-                pbyte = q == k / 4 ? pb[q] : pbyte;
-            pbyte = (pbyte >> (8 * (k & 3))) & 0xFFu;
-            if (h)
-                emit_lane(h, c0, x, pbyte, stc, stv, inc - cnt);
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            for (uint32_t j = lane; j < item_total; j += kWave) {
-                const uint64_t gi = g_item + j;
-                if (gi > 0) {
-                    counts[gi - 1] = stc[j];
-                    values[gi - 1] = stv[j];
+            for (int half = 0; half < 2; ++half) {
+                const uint64_t hm = half ? h1 : h0;
+                if ((hm >> lane) & 1u) {
+                    const uint64_t bl = hm & below;
+                    const uint32_t pos = (uint32_t)(half * 64 + lane);
+                    const uint32_t rank = (half ? (uint32_t)__popcll(h0) : 0u) + (uint32_t)__popcll(bl);
+                    int prev;
+                    if (bl)
+                        prev = half * 64 + 63 - __builtin_clzll(bl);
+                    else
+                        prev = (half && h0) ? 63 - __builtin_clzll(h0) : -1;
+                    uint32_t cnt = prev < 0 ? add_c(c_row, pos) : pos - (uint32_t)prev;
+                    cnt = cnt == 0 ? 255u : cnt;
+                    const uint32_t q = pos - 1;
+                    const uint32_t val =
+                        pos == 0 ? p_row : rowp[(((q >> 4) ^ (rr & 7u)) * 16) + (q & 15u)];
+                    const uint64_t gi = g_row + rank;
+                    if (gi > 0) {
+                        counts[gi - 1] = (uint8_t)cnt;
+                        values[gi - 1] = (uint8_t)val;
+                    }
                 }
             }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            g_item += item_total;
         }
     }
-    FLRL_RL_PHASE(5);
+    FLRL_RL_PHASE(3);
     FLRL_RL_PHASE_END();
 
     // ---- the final run (ends at byte n-1) ----------------------------------
     if (tile + 1 == ntiles && tid == 0) {
-        const uint64_t R = g0 + K;
-        const uint32_t c_end = pm_apply(tile_map, c_in);
+        const uint64_t end = sm_compose(tile_state, tile_map);
+        const uint64_t R = sm_h(end);
+        const uint32_t c_end = sm_c(end);
         counts[R - 1] = (uint8_t)(c_end == 0 ? 255u : c_end);
         values[R - 1] = in[n - 1];
         *runs_out = R;
@@ -801,7 +763,7 @@ extern "C" int flrl_rl_encode_device(const uint8_t *d_in, size_t n, uint8_t *d_c
         return set_error(FLRL_E_ARG, "flrl_rl_encode_device: input too large");
     Ctrl *ctrl = static_cast<Ctrl *>(d_scratch);
     uint64_t *status = reinterpret_cast<uint64_t *>(ctrl + 1);
-    hipLaunchKernelGGL((rl_encode_kernel<kRlThreads, kRlItems, kRlStage>), dim3((uint32_t)L.tiles),
+    hipLaunchKernelGGL((rl_encode_kernel<kRlThreads, kRlLaneBytes>), dim3((uint32_t)L.tiles),
                        dim3(kRlThreads), 0, s, d_in, (uint64_t)n, (uint32_t)L.tiles, d_counts,
                        d_values, d_runs, ctrl, status);
     FLRL_HIP(hipGetLastError());

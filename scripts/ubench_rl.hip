@@ -103,8 +103,8 @@ int main(int argc, char **argv)
 #ifdef STAMP
     unsigned long long ph[64];
     CK(hipMemcpyFromSymbol(ph, HIP_SYMBOL(g_ph), sizeof(ph)));
-    const char *names[6] = {"ticket", "load+nat+mapscan", "wavecombine+fake+sum", "lookback+barrier",
-                            "true heads+sum", "emit"};
+    const char *names[6] = {"ticket+load", "scan+publish", "lookback+barrier", "emit",
+                            "-", "-"};
     for (int w = 0; w < 4; ++w) {
         unsigned long long tot = 0;
         for (int i = 0; i < 6; ++i)
