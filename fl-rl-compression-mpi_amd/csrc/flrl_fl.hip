@@ -446,25 +446,6 @@ struct FlLayout {
     }
 };
 
-static int cu_count()
-{
-    static std::atomic<int> cache[64];
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess)
-        dev = 0;
-    if (dev >= 0 && dev < 64) {
-        const int c = cache[dev].load(std::memory_order_relaxed);
-        if (c > 0)
-            return c;
-    }
-    int c = 0;
-    if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c <= 0)
-        c = 256;
-    if (dev >= 0 && dev < 64)
-        cache[dev].store(c, std::memory_order_relaxed);
-    return c;
-}
-
 }  // namespace flrl
 
 using namespace flrl;

@@ -8,6 +8,8 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include <atomic>
+
 #include "flrl.h"
 
 namespace flrl {
@@ -43,5 +45,25 @@ struct DevBuf {
         return reinterpret_cast<T *>(static_cast<uint8_t *>(p) + byte_off);
     }
 };
+
+// Compute units of the current device (cached per device): persistent grids.
+inline int cu_count()
+{
+    static std::atomic<int> cache[64];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess)
+        dev = 0;
+    if (dev >= 0 && dev < 64) {
+        const int c = cache[dev].load(std::memory_order_relaxed);
+        if (c > 0)
+            return c;
+    }
+    int c = 0;
+    if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c <= 0)
+        c = 256;
+    if (dev >= 0 && dev < 64)
+        cache[dev].store(c, std::memory_order_relaxed);
+    return c;
+}
 
 }  // namespace flrl

@@ -9,16 +9,18 @@
 // predecessor (or is byte 0). The state c before a byte is the number of bytes
 // of the current chunk so far (1..254, with 255 written as 0); byte i is a head
 // iff it is natural or c == 0, and then c becomes 1, else c = (c+1) mod 255.
-// Within a tile, a PhaseMap scan (constant after a natural head, else
-// "+L mod 255") gives every lane's state relative to the tile's incoming one.
-// Across tiles ONE decoupled look-back composes segment maps {bytes before the
-// first natural head, heads from it on, state after} into (heads before the
-// tile, state at its start). Each head h emits the run that ENDS at h-1
-// (count = c before h, value = x[h-1]); the tile holding byte n-1 emits the
-// final run, so no tile needs bytes of its successor. Heads from a tile's first
-// natural head on do not depend on the incoming state: their runs are staged
-// in LDS before the look-back, and only the split heads before that first
-// natural head (all full 255-byte chunks) wait for it.
+// Each head h emits the run that ENDS at h-1 (count = c before h, value =
+// x[h-1]); the tile holding byte n-1 emits the final run, so no tile needs
+// bytes of its successor. A 64 KiB tile sits in LDS (LDS-DMA) and each lane
+// owns 128 contiguous bytes of it, so a lane holds at most one split head
+// (before its first natural head). Within the tile two 32-bit scans suffice: a
+// PhaseMap scan of lane states (constant after a natural head, else
+// "+L mod 255") and a sum of the heads that do not depend on the tile's
+// incoming state (those from its first natural head on). Across tiles ONE
+// decoupled look-back composes segment maps {bytes before the first natural
+// head, heads from it on, state after} into (heads before the tile, state at
+// its start); every lane then knows its global head index and state and emits
+// its runs, staged per wave in LDS and stored contiguously.
 //
 // Decode: rl_offsets_kernel scans the counts (R bytes) into per-tile output
 // offsets (and validates them); rl_decode_kernel then expands each tile of
@@ -47,7 +49,8 @@ namespace flrl {
 constexpr int kRlThreads = 512;                     // encode workgroup: 8 waves
 constexpr int kRlLaneBytes = 128;                   // contiguous bytes per lane
 constexpr int kRlTileBytes = kRlLaneBytes * kRlThreads;  // 64 KiB, held in LDS
-constexpr int kRlDenseRun = 32;  // > this many heads per lane (mean run < 4 B): row-wise emission
+constexpr int kRlLookG = 1;      // look-back granules per lane (window 64 G tiles)
+constexpr int kRlStageBytes = 16256;  // LDS run staging (2 workgroups of 64 KiB tiles per CU)
 
 constexpr int kRdRuns = 4096;        // runs per decode tile
 constexpr int kRdThreads = 256;
@@ -106,31 +109,27 @@ __device__ __forceinline__ uint32_t nat_mask(u32x4 x, uint32_t p)
     return m;
 }
 
-__device__ __forceinline__ uint32_t byte_at(u32x4 x, uint32_t i)
-{
-    const uint64_t lo = ((uint64_t)x.y << 32) | x.x, hi = ((uint64_t)x.w << 32) | x.z;
-    return (uint32_t)((i < 8 ? lo >> (8 * i) : hi >> (8 * (i - 8))) & 0xFFu);
-}
-
 // ---- composite segment map for the single tile look-back -------------------
 // Acting on the state (H = heads before, c = chunk state) at a segment start:
 //   kind NoNat (L):       H += splits(c, L);        c = (c + L) mod 255
 //   kind Nat (pre, K, ca): H += splits(c, pre) + K;  c = ca
 //   kind Const (H, c):    the state itself (an inclusive prefix)
-// splits(c, m) = #{j < m : (c + j) mod 255 == 0}. Packed in 56 bits: c in 0-7,
-// pre/L in 8-30, K in 31-53, kind in 54-55; Const keeps H in bits 8-53.
-constexpr uint64_t kSmNat = 1ull << 54, kSmConst = 2ull << 54, kSmKind = 3ull << 54;
+// splits(c, m) = #{j < m : (c + j) mod 255 == 0}. Packed in the 62 payload bits
+// of a status granule: c in 0-7, pre/L in 8-33, K in 34-59, kind in 60-61;
+// Const keeps H in bits 8-59.
+constexpr uint64_t kSmNat = 1ull << 60, kSmConst = 2ull << 60, kSmKind = 3ull << 60;
+constexpr uint32_t kSmField = (1u << 26) - 1;
 __device__ __forceinline__ uint64_t sm_nonat(uint32_t L) { return (uint64_t)L << 8; }
 __device__ __forceinline__ uint64_t sm_nat(uint32_t pre, uint32_t K, uint32_t c)
 {
-    return kSmNat | ((uint64_t)K << 31) | ((uint64_t)pre << 8) | c;
+    return kSmNat | ((uint64_t)K << 34) | ((uint64_t)pre << 8) | c;
 }
 __device__ __forceinline__ uint64_t sm_const(uint64_t H, uint32_t c) { return kSmConst | (H << 8) | c; }
 __device__ __forceinline__ uint32_t sm_c(uint64_t m) { return (uint32_t)(m & 0xFFu); }
-__device__ __forceinline__ uint32_t sm_a(uint64_t m) { return (uint32_t)(m >> 8) & 0x7FFFFFu; }
-__device__ __forceinline__ uint32_t sm_b(uint64_t m) { return (uint32_t)(m >> 31) & 0x7FFFFFu; }
-__device__ __forceinline__ uint64_t sm_h(uint64_t m) { return (m >> 8) & ((1ull << 46) - 1); }
-// 32-bit forms for packed (< 2^23) lengths; the 64-bit ones only for the
+__device__ __forceinline__ uint32_t sm_a(uint64_t m) { return (uint32_t)(m >> 8) & kSmField; }
+__device__ __forceinline__ uint32_t sm_b(uint64_t m) { return (uint32_t)(m >> 34) & kSmField; }
+__device__ __forceinline__ uint64_t sm_h(uint64_t m) { return (m >> 8) & ((1ull << 52) - 1); }
+// 32-bit forms for packed (< 2^26) lengths; the 64-bit ones only for the
 // cross-window accumulator of the look-back
 __device__ __forceinline__ uint32_t splits(uint32_t c, uint32_t m)
 {
@@ -168,11 +167,15 @@ __device__ __forceinline__ uint64_t sm_compose(uint64_t a, uint64_t b)
 }
 
 // Look-back for (H, c), run by ONE wave after the tile published its composite
-// map (A; tile 0 publishes its inclusive prefix P instead): compose the window
-// from the nearest P forward (6-level shuffle tree), publish this tile's P,
-// return the Const state at the tile start. Windows hold <= 64 tiles of
-// <= 64 KiB, so packed fields of composed window maps fit; across windows the
-// accumulator is kept unpacked.
+// map (A; tile 0 publishes its inclusive prefix P instead). Each lane loads G
+// granules at once (tiles j-G*lane .. j-G*lane-G+1), so one round trip covers
+// 64*G predecessors: a persistent grid of one workgroup per CU has about that
+// many tiles in flight, all at the same stage, and a 64-wide window would need
+// several dependent round trips to reach the last inclusive prefix (P). The
+// window is composed from its nearest P forward (per lane, then a 6-level
+// shuffle tree), this tile's P is published and the Const state at the tile
+// start returned. Composed window maps span <= 64*G tiles of <= 64 KiB, within
+// the 26-bit packed fields; across windows the accumulator is kept unpacked.
 __device__ __forceinline__ void publish_seg(uint64_t *status, uint32_t tile, uint64_t map)
 {
     if ((threadIdx.x & (kWave - 1)) == 0)
@@ -180,11 +183,12 @@ __device__ __forceinline__ void publish_seg(uint64_t *status, uint32_t tile, uin
                                                : (kFlagA | map));
 }
 
+template <int G>
 __device__ __forceinline__ uint64_t lookback_seg(uint64_t *status, uint32_t tile, uint64_t map,
                                                  Ctrl *ctrl)
 {
     const int lane = threadIdx.x & (kWave - 1);
-    const uint64_t kPay = (1ull << 56) - 1;
+    const uint64_t kPay = (1ull << 62) - 1;
     if (tile == 0)
         return sm_const(0, 0);
     // accumulator for windows without an inclusive prefix (newest part), unpacked
@@ -194,11 +198,36 @@ __device__ __forceinline__ uint64_t lookback_seg(uint64_t *status, uint32_t tile
     int64_t j = (int64_t)tile - 1;
     uint32_t spins = 0;
     for (;;) {
-        const int64_t idx = j - lane;
-        uint64_t s;
+        const int64_t idx = j - (int64_t)lane * G;
+        uint64_t s[G];
+        uint64_t m;
+        bool has_p;
         for (;;) {
-            s = idx >= 0 ? granule_load(&status[idx]) : (kFlagP | sm_const(0, 0));
-            if (window_ready(s))
+#pragma unroll
+            for (int k = 0; k < G; ++k)
+                s[k] = idx - k >= 0 ? granule_load(&status[idx - k]) : (kFlagP | sm_const(0, 0));
+            // lane-local: compose from the lane's nearest P (or its oldest
+            // granule) forward; ready if nothing up to that P is unpublished
+            has_p = false;
+            bool ok = true;
+            m = sm_nonat(0);
+#pragma unroll
+            for (int k = 0; k < G; ++k) {
+                if (!has_p) {
+                    const uint32_t f = (uint32_t)(s[k] >> 62);
+                    ok = ok && f != 0;
+                    if (f == 2) {
+                        has_p = true;
+                        m = sm_compose(sm_const(sm_h(s[k]), sm_c(s[k])), m);
+                    } else {
+                        m = sm_compose(s[k] & kPay, m);
+                    }
+                }
+            }
+            const unsigned long long pm = __ballot(has_p);
+            const unsigned long long bad = __ballot(!ok);
+            const unsigned long long upto = pm ? ((pm & (~pm + 1)) << 1) - 1 : ~0ull;
+            if ((bad & upto) == 0)
                 break;
             if (++spins > kSpinLimit) {
                 if (lane == 0)
@@ -207,9 +236,10 @@ __device__ __forceinline__ uint64_t lookback_seg(uint64_t *status, uint32_t tile
             }
             __builtin_amdgcn_s_sleep(1);
         }
-        const unsigned long long pm = __ballot((s >> 62) == 2);
+        const unsigned long long pm = __ballot(has_p);
         const int first = pm ? __ffsll(pm) - 1 : kWave;
-        uint64_t m = lane < first ? (s & kPay) : (lane == first ? sm_const(sm_h(s), sm_c(s)) : 0ull);
+        if (lane > first)
+            m = sm_nonat(0);
         // suffix composition: lane l ends with compose(m_63 .. m_l); identity = no-nat L 0
 #pragma unroll
         for (int o = 1; o < kWave; o <<= 1) {
@@ -249,51 +279,21 @@ __device__ __forceinline__ uint64_t lookback_seg(uint64_t *status, uint32_t tile
         } else {
             acc_a = sm_a(win) + acc_a;
         }
-        j -= kWave;
+        j -= (int64_t)kWave * G;
     }
 }
 
-// Heads of one lane-item given the chunk state c0 before its first byte: the
-// natural heads, plus at most one split head where the state first wraps to 0
-// (offset j0 = (255 - c0) mod 255), if no natural head comes at or before it.
-// After any head the state restarts at 1, so a second split needs 255 more bytes.
-__device__ __forceinline__ uint32_t lane_heads(uint32_t nat, uint32_t c0, uint32_t vb)
-{
-    const uint32_t j0 = c0 == 0 ? 0u : 255u - c0;
-    const uint32_t below = (1u << (j0 & 15)) - 1u;
-    const bool split = j0 < vb && (nat & below) == 0;
-    return nat | (split ? 1u << (j0 & 15) : 0u);
-}
-
-// Block-wide (T threads) exclusive sum; returns the exclusive prefix of v and
-// the total in *total. Uses s_w[T/64]; two barriers.
-template <int T>
-__device__ __forceinline__ uint32_t block_excl_sum(uint32_t v, uint32_t *s_w, uint32_t *total)
-{
-    const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
-    const uint32_t inc = wave_incl_scan_u32(v);
-    if (lane == kWave - 1)
-        s_w[w] = inc;
-    __syncthreads();
-    uint32_t before = 0, tot = 0;
-#pragma unroll
-    for (int i = 0; i < T / kWave; ++i) {
-        before += i < w ? s_w[i] : 0u;
-        tot += s_w[i];
-    }
-    __syncthreads();
-    *total = tot;
-    return before + inc - v;
-}
-
-// One tile of T/64 x 64 lanes x LB bytes per workgroup, in ticket order. The
-// tile lands in LDS by LDS-DMA (global_load_lds, 1 KiB per wave-instruction,
-// coalesced), swizzled so that every lane can then read ITS OWN contiguous LB
-// bytes conflict-free: lane row r keeps chunk c at r*LB + ((c ^ (r & 7)) * 16).
-// Each lane folds its bytes into one segment map (so a wave needs ONE scan,
-// not one per chunk), the tile's map goes through the look-back, and every lane
-// then knows (global head index, chunk state) at its first byte and emits its
-// own runs in order, re-reading its bytes from LDS.
+// One tile of T/64 waves x 64 lanes x LB bytes per workgroup, in ticket order.
+// The tile lands in LDS by LDS-DMA (global_load_lds, 1 KiB per wave-instruction,
+// coalesced), swizzled so that every lane then reads ITS OWN contiguous LB bytes
+// conflict-free: lane row r keeps chunk c at r*LB + ((c ^ (r & 7)) * 16).
+// Per lane: natural-head masks, count, first/last natural head. LB < 255, so a
+// lane holds at most one split head, and only before its first natural head;
+// lane phase maps and the counts of state-independent heads (those from the
+// tile's first natural head on) then need two cheap 32-bit wave scans. The
+// tile's composite map goes through the look-back; every lane then knows its
+// global head index and chunk state and emits its runs in order: staged per
+// wave in LDS and stored contiguously, or (dense waves) one lane row at a time.
 template <int T, int LB>
 __global__ __launch_bounds__(T) void rl_encode_kernel(
     const uint8_t *__restrict__ in, uint64_t n, uint32_t ntiles, uint8_t *__restrict__ counts,
@@ -303,26 +303,33 @@ __global__ __launch_bounds__(T) void rl_encode_kernel(
     constexpr int CH = LB / 16;  // 16-byte chunks per lane
     constexpr int WB = kWave * LB;
     constexpr int TB = WB * W;
+    constexpr int SW = kRlStageBytes / W / 2;  // staged records per wave
     static_assert(LB == 128, "the swizzle and the 2 x u64 head masks assume 8 chunks per lane");
-    __shared__ __attribute__((aligned(16))) uint8_t s_data[TB];
-    __shared__ uint64_t s_wmap[W];
-    __shared__ uint32_t s_ticket;
-    __shared__ uint64_t s_state;
+    // ONE LDS object: [tile image][per-wave staging: counts | values][small]
+    __shared__ __attribute__((aligned(16))) uint8_t s_lds[TB + kRlStageBytes + 128];
+    uint8_t *const img = s_lds;
+    uint8_t *const stc = s_lds + TB + (size_t)(threadIdx.x / kWave) * 2 * SW;
+    uint8_t *const stv = stc + SW;
+    uint32_t *const s_wmap = reinterpret_cast<uint32_t *>(s_lds + TB + kRlStageBytes);
+    uint32_t *const s_wfirst = s_wmap + W;
+    uint32_t *const s_wh = s_wfirst + W;
+    uint32_t *const s_ticket = s_wh + W;
+    uint64_t *const s_state = reinterpret_cast<uint64_t *>(s_lds + TB + kRlStageBytes + 120);
+    static_assert(3 * W * 4 + 4 <= 120, "small LDS fields");
 
     const int tid = threadIdx.x;
     const int lane = tid & (kWave - 1);
     const int w = tid / kWave;
     FLRL_RL_PHASE_BEGIN();
-    const uint32_t tile = take_ticket(ctrl, &s_ticket);
+    const uint32_t tile = take_ticket(ctrl, s_ticket);
     const uint64_t tile_off = (uint64_t)tile * TB;
     const uint64_t wave_off = tile_off + (uint64_t)w * WB;
 
     // ---- tile -> LDS. Instruction j of wave w fills rows w*64 + j*8 .. +7;
     // lane writes row j*8 + lane/8 at column lane&7, i.e. chunk (lane&7)^(row&7)
     {
-        const uint32_t col = (uint32_t)lane & 7u;
-        const uint32_t c = col ^ (((uint32_t)lane >> 3) & 7u);
-        uint8_t *dst = s_data + w * WB;
+        const uint32_t c = ((uint32_t)lane & 7u) ^ (((uint32_t)lane >> 3) & 7u);
+        uint8_t *dst = img + w * WB;
         if (wave_off + WB <= n) {
 #pragma unroll
             for (int j = 0; j < WB / 1024; ++j) {
@@ -340,22 +347,22 @@ __global__ __launch_bounds__(T) void rl_encode_kernel(
         }
     }
     const uint32_t row = (uint32_t)tid;  // lane row within the tile
-    const uint64_t lane_off = tile_off + (uint64_t)row * LB;
+    const uint32_t o = row * LB;          // its byte offset in the tile
+    const uint64_t lane_off = tile_off + o;
     const uint32_t vbl = lane_off >= n ? 0u : (n - lane_off >= LB ? (uint32_t)LB : (uint32_t)(n - lane_off));
     const uint32_t ptile = (tid == 0 && tile_off > 0) ? in[tile_off - 1] : 0u;
     __syncthreads();  // waits for the LDS-DMA too
     FLRL_RL_PHASE(0);
 
-    const uint8_t *my = s_data + row * LB;
+    const uint8_t *my = img + o;
     auto chunk = [&](int c) -> u32x4 {
         return *reinterpret_cast<const u32x4 *>(my + ((c ^ (row & 7u)) * 16));
     };
-    const uint32_t p0 = row == 0 ? ptile : s_data[(row - 1) * LB + ((7u ^ ((row - 1) & 7u)) * 16) + 15];
+    const uint32_t p0 = row == 0 ? ptile : img[(row - 1) * LB + ((7u ^ ((row - 1) & 7u)) * 16) + 15];
 
-    // ---- pass 1: natural heads and the lane's segment map -----------------
+    // ---- pass 1: natural heads ----------------------------------------------
     uint32_t nat[CH / 2];  // 16-bit masks, two per word
-    bool has = false;
-    uint32_t pre = 0, K = 0, cs = 0;
+    uint32_t ncnt = 0, fpos = LB, lpos = 0;
     {
         uint32_t p = p0;
 #pragma unroll
@@ -370,86 +377,106 @@ __global__ __launch_bounds__(T) void rl_encode_kernel(
             else
                 nat[c / 2] = m;
             p = x.w >> 24;
-            if (!has) {
-                if (m) {
-                    has = true;
-                    pre += __ffs(m) - 1;
-                    K = __popc(m);
-                    cs = vb - (31u - __clz(m));
-                } else {
-                    pre += vb;
-                }
-            } else {
-                const uint32_t h = lane_heads(m, cs, vb);
-                K += __popc(h);
-                cs = h ? vb - (31u - __clz(h)) : add_c(cs, vb);
+            ncnt += __popc(m);
+            if (m) {
+                fpos = fpos == (uint32_t)LB ? 16u * c + (__ffs(m) - 1) : fpos;
+                lpos = 16u * c + (31u - __clz(m));
             }
         }
     }
-    const uint64_t lmap = has ? sm_nat(pre, K, cs) : sm_nonat(pre);
-
-    // ---- lane -> wave -> tile scans of segment maps ------------------------
-    uint64_t incl = lmap;
-#pragma unroll
-    for (int o = 1; o < kWave; o <<= 1) {
-        const uint64_t up = __shfl_up(incl, o, kWave);
-        if (lane >= o)
-            incl = sm_compose(up, incl);
+    const bool has = ncnt != 0;
+    // lane phase map, wave scan (exclusive), first natural head of the wave
+    const uint32_t lmap = has ? pm_make(true, vbl - lpos) : pm_make(false, vbl);
+    const uint32_t incl = wave_incl_scan_map(lmap);
+    uint32_t lexcl = __shfl_up(incl, 1, kWave);
+    lexcl = lane == 0 ? kMapIdent : lexcl;
+    {
+        const unsigned long long hb = __ballot(has);
+        const int fl = hb ? __ffsll(hb) - 1 : 0;
+        const uint32_t ff = (uint32_t)__shfl(fpos, fl, kWave);
+        if (lane == kWave - 1)
+            s_wmap[w] = incl;
+        if (lane == 0)
+            s_wfirst[w] = hb ? (uint32_t)(w * WB + fl * LB) + ff : 0xFFFFFFFFu;
     }
-    uint64_t lane_pre = __shfl_up(incl, 1, kWave);
-    if (lane == 0)
-        lane_pre = sm_nonat(0);
-    if (lane == kWave - 1)
-        s_wmap[w] = incl;
     __syncthreads();
-    uint64_t tile_map = sm_nonat(0), wave_pre = sm_nonat(0);
+    uint32_t tile_map = kMapIdent, wave_pre = kMapIdent, tile_first = 0xFFFFFFFFu;
 #pragma unroll
     for (int v = 0; v < W; ++v) {
         if (v == w)
             wave_pre = tile_map;
-        tile_map = sm_compose(tile_map, s_wmap[v]);
+        tile_map = pm_compose(tile_map, s_wmap[v]);
+        if (tile_first == 0xFFFFFFFFu && s_wfirst[v] != 0xFFFFFFFFu)
+            tile_first = s_wfirst[v];
     }
-    if (w == 0)
-        publish_seg(status, tile, tile_map);
+    const uint32_t tile_len = (uint32_t)(n - tile_off < (uint64_t)TB ? n - tile_off : TB);
+    const uint32_t lane_rel = pm_compose(wave_pre, lexcl);  // lane start state from the tile's
+
+    // ---- heads that do not depend on the tile's incoming state: all heads from
+    // the tile's first natural head on. After it, lane start states are
+    // constants of the scan; the lane holding it counts its natural heads only.
+    uint32_t indep = 0;
+    if (tile_first != 0xFFFFFFFFu && o + LB > tile_first) {
+        indep = ncnt;
+        if (o > tile_first) {
+            const uint32_t cr = pm_apply(lane_rel, 1);  // any stand-in incoming state
+            const uint32_t j0 = cr == 0 ? 0u : 255u - cr;
+            indep += (j0 < fpos && j0 < vbl) ? 1u : 0u;
+        }
+    }
+    const uint32_t hincl = wave_incl_scan_u32(indep);
+    if (lane == kWave - 1)
+        s_wh[w] = hincl;
+    __syncthreads();
+    uint32_t K = 0, wave_hbase = 0;
+#pragma unroll
+    for (int v = 0; v < W; ++v) {
+        wave_hbase += v < w ? s_wh[v] : 0u;
+        K += s_wh[v];
+    }
+    const uint32_t pre = K ? tile_first : tile_len;
+    const uint64_t tmap = K ? sm_nat(tile_first, K, tile_map & 0xFFu) : sm_nonat(tile_len);
     FLRL_RL_PHASE(1);
 
     // ---- one look-back: (heads before the tile, chunk state at its start) --
     if (w == 0) {
-        const uint64_t state = lookback_seg(status, tile, tile_map, ctrl);
+        publish_seg(status, tile, tmap);
+        const uint64_t state = lookback_seg<kRlLookG>(status, tile, tmap, ctrl);
         if (lane == 0)
-            s_state = state;
+            *s_state = state;
     }
     __syncthreads();
     FLRL_RL_PHASE(2);
-    const uint64_t tile_state = s_state;
-    const uint64_t lane_state = sm_compose(sm_compose(tile_state, wave_pre), lane_pre);
-    uint64_t g = sm_h(lane_state);  // global index of the lane's next head
-    const uint32_t c_lane = sm_c(lane_state);
+    const uint64_t h_in = sm_h(*s_state);
+    const uint32_t c_in = sm_c(*s_state);
+    const uint32_t c_lane = pm_apply(lane_rel, c_in);
+    uint64_t g = (K && o > tile_first) ? h_in + splits(c_in, pre) + wave_hbase + (hincl - indep)
+                                       : h_in + splits(c_in, o);
 
-    // ---- heads with the true states, then the lane's runs in order ----------
-    uint64_t hm0 = 0, hm1 = 0;  // head masks of chunks 0-3 / 4-7
+    // ---- head masks with the true states, then the lane's runs in order -----
+    uint64_t hm0 = 0, hm1 = 0;  // chunks 0-3 / 4-7
     {
-        uint32_t cst = c_lane;
+        const uint32_t j0 = c_lane == 0 ? 0u : 255u - c_lane;
+        const bool split = j0 < fpos && j0 < vbl;
 #pragma unroll
         for (int c = 0; c < CH; ++c) {
-            const uint32_t vb = vbl > 16u * c ? (vbl - 16u * c >= 16 ? 16u : vbl - 16u * c) : 0u;
-            const uint32_t m = (nat[c / 2] >> (16 * (c & 1))) & 0xFFFFu;
-            const uint32_t h = lane_heads(m, cst, vb);
-            cst = h ? vb - (31u - __clz(h)) : add_c(cst, vb);
+            uint32_t h = (nat[c / 2] >> (16 * (c & 1))) & 0xFFFFu;
+            if (split && (j0 >> 4) == (uint32_t)c)
+                h |= 1u << (j0 & 15u);
             if (c < 4)
                 hm0 |= (uint64_t)h << (16 * c);
             else
                 hm1 |= (uint64_t)h << (16 * (c - 4));
         }
     }
-    // Sparse heads (compressible data): every lane walks its own heads; a
-    // wave-instruction's stores then span a few hundred bytes. Dense heads: the
-    // lanes' ranges are far apart, so the wave emits ONE lane row at a time,
-    // lane t taking byte positions t and 64 + t of the row (ranks by popcount),
-    // which keeps every store instruction contiguous.
-    const uint32_t wave_heads =
-        (uint32_t)wave_sum_u64((uint64_t)(__popcll(hm0) + __popcll(hm1)));
-    if (wave_heads <= (uint32_t)(kRlDenseRun * kWave)) {
+    const uint32_t lane_heads_n = (uint32_t)(__popcll(hm0) + __popcll(hm1));
+    const uint32_t wave_heads = (uint32_t)wave_sum_u64((uint64_t)lane_heads_n);
+    if (wave_heads <= (uint32_t)SW) {
+        // sparse: each lane stages its runs at (g - first g of the wave) in LDS,
+        // then the wave stores them contiguously
+        const uint64_t gw = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(g >> 32), 0) << 32) |
+                            (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)g, 0);
+        uint32_t slot = (uint32_t)(g - gw);
         int prev = -1;  // position of the previous head in this lane
         while (hm0 | hm1) {
             int pos;
@@ -469,14 +496,25 @@ __global__ __launch_bounds__(T) void rl_encode_kernel(
                 const uint32_t q = (uint32_t)pos - 1;
                 val = my[(((q >> 4) ^ (row & 7u)) * 16) + (q & 15u)];
             }
-            if (g > 0) {
-                counts[g - 1] = (uint8_t)cnt;
-                values[g - 1] = (uint8_t)val;
-            }
-            ++g;
+            stc[slot] = (uint8_t)cnt;
+            stv[slot] = (uint8_t)val;
+            ++slot;
             prev = pos;
         }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        for (uint32_t j = lane; j < wave_heads; j += kWave) {
+            const uint64_t gi = gw + j;
+            if (gi > 0) {
+                counts[gi - 1] = stc[j];
+                values[gi - 1] = stv[j];
+            }
+        }
     } else {
+        // dense: the wave emits ONE lane row at a time, lane t taking byte
+        // positions t and 64 + t of the row (ranks by popcount), so every
+        // store instruction stays contiguous
         const uint64_t below = ((uint64_t)1 << lane) - 1;
 #pragma unroll 1
         for (int r = 0; r < kWave; ++r) {
@@ -489,7 +527,7 @@ __global__ __launch_bounds__(T) void rl_encode_kernel(
             const uint32_t c_row = (uint32_t)__builtin_amdgcn_readlane((int)c_lane, r);
             const uint32_t p_row = (uint32_t)__builtin_amdgcn_readlane((int)p0, r);
             const uint32_t rr = (uint32_t)(w * kWave + r);
-            const uint8_t *rowp = s_data + rr * LB;
+            const uint8_t *rowp = img + rr * LB;
 #pragma unroll
             for (int half = 0; half < 2; ++half) {
                 const uint64_t hm = half ? h1 : h0;
@@ -505,8 +543,7 @@ __global__ __launch_bounds__(T) void rl_encode_kernel(
                     uint32_t cnt = prev < 0 ? add_c(c_row, pos) : pos - (uint32_t)prev;
                     cnt = cnt == 0 ? 255u : cnt;
                     const uint32_t q = pos - 1;
-                    const uint32_t val =
-                        pos == 0 ? p_row : rowp[(((q >> 4) ^ (rr & 7u)) * 16) + (q & 15u)];
+                    const uint32_t val = pos == 0 ? p_row : rowp[(((q >> 4) ^ (rr & 7u)) * 16) + (q & 15u)];
                     const uint64_t gi = g_row + rank;
                     if (gi > 0) {
                         counts[gi - 1] = (uint8_t)cnt;
@@ -521,9 +558,8 @@ __global__ __launch_bounds__(T) void rl_encode_kernel(
 
     // ---- the final run (ends at byte n-1) ----------------------------------
     if (tile + 1 == ntiles && tid == 0) {
-        const uint64_t end = sm_compose(tile_state, tile_map);
-        const uint64_t R = sm_h(end);
-        const uint32_t c_end = sm_c(end);
+        const uint64_t R = h_in + splits(c_in, pre) + K;
+        const uint32_t c_end = pm_apply(tile_map, c_in);
         counts[R - 1] = (uint8_t)(c_end == 0 ? 255u : c_end);
         values[R - 1] = in[n - 1];
         *runs_out = R;
@@ -763,9 +799,8 @@ extern "C" int flrl_rl_encode_device(const uint8_t *d_in, size_t n, uint8_t *d_c
         return set_error(FLRL_E_ARG, "flrl_rl_encode_device: input too large");
     Ctrl *ctrl = static_cast<Ctrl *>(d_scratch);
     uint64_t *status = reinterpret_cast<uint64_t *>(ctrl + 1);
-    hipLaunchKernelGGL((rl_encode_kernel<kRlThreads, kRlLaneBytes>), dim3((uint32_t)L.tiles),
-                       dim3(kRlThreads), 0, s, d_in, (uint64_t)n, (uint32_t)L.tiles, d_counts,
-                       d_values, d_runs, ctrl, status);
+    hipLaunchKernelGGL((rl_encode_kernel<kRlThreads, kRlLaneBytes>), dim3((uint32_t)L.tiles), dim3(kRlThreads), 0, s,
+                       d_in, (uint64_t)n, (uint32_t)L.tiles, d_counts, d_values, d_runs, ctrl, status);
     FLRL_HIP(hipGetLastError());
     return FLRL_OK;
 }

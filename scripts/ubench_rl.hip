@@ -103,7 +103,7 @@ int main(int argc, char **argv)
 #ifdef STAMP
     unsigned long long ph[64];
     CK(hipMemcpyFromSymbol(ph, HIP_SYMBOL(g_ph), sizeof(ph)));
-    const char *names[6] = {"ticket+load", "scan+publish", "lookback+barrier", "emit",
+    const char *names[6] = {"load", "scan", "lookback+barrier", "emit",
                             "-", "-"};
     for (int w = 0; w < 4; ++w) {
         unsigned long long tot = 0;
