@@ -132,6 +132,11 @@ __device__ __forceinline__ void stage_packed(uint8_t *s, uint32_t off, uint32_t 
 // issues its share of the prefetch only after its look-back: vmcnt is per wave
 // and in order, so status loads issued behind 16 bulk loads would each wait
 // for all of them (measured: scripts/ubench_encode.hip).
+// Per-tile timestamp hook for scripts/ubench_fl.hip (no-op in the library).
+#ifndef FLRL_FL_TRACE
+#define FLRL_FL_TRACE(tile, k) ((void)0)
+#endif
+
 template <int T, int ITEMS>
 __global__ __launch_bounds__(T, 1) void fl_encode_kernel(
     const uint8_t *__restrict__ in, uint64_t n, uint64_t nframes, uint32_t ntiles,
@@ -164,6 +169,7 @@ __global__ __launch_bounds__(T, 1) void fl_encode_kernel(
         __syncthreads();  // previous tile's LDS readers are done; s_next consumed
         if (tid == 0)
             s_next = atomicAdd(&ctrl->ticket, 1u);  // next ticket, read after the barrier below
+        FLRL_FL_TRACE(tile, 0);
         const uint64_t frame0 = (uint64_t)tile * TF;
 
         // ---- frame widths: OR over the frame's 8 lanes, b = max(1, bitlen)
@@ -190,6 +196,7 @@ __global__ __launch_bounds__(T, 1) void fl_encode_kernel(
         // ---- publish the tile's width sum early (successors' look-backs need it)
         if (tid == 0)
             publish_aggregate(status, tile, agg);
+        FLRL_FL_TRACE(tile, 1);
 
         // ---- bits[] for this tile's frames
         if (frame0 + TF <= nframes) {
@@ -228,6 +235,7 @@ __global__ __launch_bounds__(T, 1) void fl_encode_kernel(
             const uint64_t excl = lookback_resolve(status, tile, agg, ctrl);
             if (tid == 0)
                 s_base = excl;
+            FLRL_FL_TRACE(tile, 2);
             if (more)
                 load_tile<T, ITEMS>(a, in, (uint64_t)nxt * TB, n);
         }
@@ -255,6 +263,7 @@ __global__ __launch_bounds__(T, 1) void fl_encode_kernel(
             for (uint32_t c = tid; c < agg; c += T)
                 store16_tail(values, 16ull * (base + c), vsize, s_out[c]);
         }
+        FLRL_FL_TRACE(tile, 3);
         if (!more)
             break;
         tile = nxt;

@@ -1,0 +1,28 @@
+"""Summarise a per-tile timestamp trace written by scripts/ubench_{fl,rl}.bin -DTRACE:
+u64[tiles][4] s_memrealtime (100 MHz) at tile start / aggregate published /
+look-back resolved / stores issued."""
+import sys
+
+import numpy as np
+
+t = np.fromfile(sys.argv[1], dtype=np.uint64).reshape(-1, 4).astype(np.int64)
+t0 = t[t > 0].min()
+t = (t - t0) * 10 / 1000.0  # us
+start, pub, lb, end = t[:, 0], t[:, 1], t[:, 2], t[:, 3]
+print(f"tiles {len(t)}  span {end.max() - start.min():.1f} us")
+
+
+def pct(x, name):
+    print(f"{name:34s} p10 {np.percentile(x, 10):7.2f}  p50 {np.percentile(x, 50):7.2f}  "
+          f"p90 {np.percentile(x, 90):7.2f}  mean {x.mean():7.2f}")
+
+
+pct(pub - start, "start -> aggregate published")
+pct(lb - pub, "published -> look-back resolved")
+pct(end - lb, "resolved -> stores issued")
+pct(pub[1:] - pub[:-1], "pub[t] - pub[t-1]")
+print("fraction of tiles whose predecessor published later:", round(float((pub[:-1] > pub[1:]).mean()), 3))
+pct(lb[1:] - lb[:-1], "lb[t] - lb[t-1]")
+i = len(t) // 2
+for k in range(i, i + 10):
+    print(k, *(round(float(v), 2) for v in t[k]))
