@@ -1,0 +1,495 @@
+// flrl_stream.hip — FL file codec streamed through one or more GPUs.
+//
+// the reference CLI loads the whole file, encodes it
+// with synchronous copies (fl_gpu.cu:330,393-394) and, for fl-mpi / fl-nccl,
+// loads per-rank shards (file_io.cu:28-71) and gathers everything to rank 0; it
+// has no multi-GPU decode (main.cu:139-147). Here a file is cut into
+// frame-aligned chunks that `workers` pipelines (one host thread each, worker w
+// on device w % devices) take round robin:
+//   compress   pread chunk -> H2D -> flrl_fl_encode_device -> D2H bits/values,
+//              two chunks in flight per worker on two streams (a chunk's D2H
+//              overlaps the next chunk's read and H2D); a writer places bits at
+//              24 + chunk_start/128 and values at 24 + F + (values of earlier
+//              chunks) with pwrite, in chunk order, and writes the header last.
+//   decompress header + bits are read once; value offsets of every chunk come
+//              from a host prefix over the widths (16 bytes per full frame);
+//              each chunk is then decoded independently and pwritten at its
+//              input offset.
+// Chunks are frame-aligned, so the file is byte-identical to a whole-input
+// encode (the concatenation identity). Memory is bounded
+// by the chunk size (per worker: 2 x (2 chunks + chunk/128) pinned host bytes
+// and as much device memory), so files larger than host RAM or HBM stream.
+#include <fcntl.h>
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <atomic>
+#include <condition_variable>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "flrl.h"
+#include "flrl_internal.hpp"
+
+namespace flrl {
+namespace {
+
+constexpr size_t kDefaultChunk = 64ull << 20;  // 64 MiB per chunk
+constexpr size_t kHeader = 24;
+constexpr size_t kFrame = FLRL_FRAME_LENGTH;
+
+// First failure of any thread, re-raised on the calling thread.
+struct Failure {
+    std::mutex m;
+    std::atomic<bool> failed{false};
+    int code = FLRL_OK;
+    std::string msg;
+    void set(int c, const std::string &s)
+    {
+        std::lock_guard<std::mutex> g(m);
+        if (!failed.load()) {
+            code = c;
+            msg = s;
+            failed.store(true);
+        }
+    }
+};
+
+struct Fd {
+    int fd = -1;
+    ~Fd()
+    {
+        if (fd >= 0)
+            ::close(fd);
+    }
+};
+
+bool pread_all(int fd, void *dst, size_t bytes, uint64_t off)
+{
+    uint8_t *p = static_cast<uint8_t *>(dst);
+    while (bytes) {
+        const ssize_t r = ::pread(fd, p, bytes, (off_t)off);
+        if (r <= 0)
+            return false;
+        p += r;
+        bytes -= (size_t)r;
+        off += (uint64_t)r;
+    }
+    return true;
+}
+
+bool pwrite_all(int fd, const void *src, size_t bytes, uint64_t off)
+{
+    const uint8_t *p = static_cast<const uint8_t *>(src);
+    while (bytes) {
+        const ssize_t r = ::pwrite(fd, p, bytes, (off_t)off);
+        if (r <= 0)
+            return false;
+        p += r;
+        bytes -= (size_t)r;
+        off += (uint64_t)r;
+    }
+    return true;
+}
+
+size_t chunk_size(size_t requested)
+{
+    size_t c = requested ? requested : kDefaultChunk;
+    c -= c % kFrame;
+    return c ? c : kFrame;
+}
+
+int worker_count(int workers, int *ndev)
+{
+    *ndev = 0;
+    if (hipGetDeviceCount(ndev) != hipSuccess || *ndev <= 0)
+        return 0;
+    return workers > 0 ? workers : *ndev;
+}
+
+// Per-worker buffers: two slots, each with its stream, pinned host staging and
+// device buffers.
+struct Slot {
+    hipStream_t s = nullptr;
+    uint8_t *h_a = nullptr, *h_b = nullptr, *h_c = nullptr;  // pinned
+    uint64_t *h_u64 = nullptr;                               // pinned
+    uint8_t *d_a = nullptr, *d_b = nullptr, *d_c = nullptr;
+    uint64_t *d_u64 = nullptr;
+    void *d_scr = nullptr;
+    size_t scr_bytes = 0;
+};
+
+struct Slots {
+    Slot slot[2];
+    ~Slots()
+    {
+        for (Slot &x : slot) {
+            if (x.s)
+                (void)hipStreamSynchronize(x.s);
+            (void)hipHostFree(x.h_a);
+            (void)hipHostFree(x.h_b);
+            (void)hipHostFree(x.h_c);
+            (void)hipHostFree(x.h_u64);
+            (void)hipFree(x.d_a);
+            (void)hipFree(x.d_b);
+            (void)hipFree(x.d_c);
+            (void)hipFree(x.d_u64);
+            (void)hipFree(x.d_scr);
+            if (x.s)
+                (void)hipStreamDestroy(x.s);
+        }
+    }
+    // a, b, c: byte capacities of the three buffer pairs
+    hipError_t alloc(size_t a, size_t b, size_t c, size_t scr)
+    {
+        for (Slot &x : slot) {
+            hipError_t e;
+            if ((e = hipStreamCreateWithFlags(&x.s, hipStreamNonBlocking)) != hipSuccess ||
+                (e = hipHostMalloc((void **)&x.h_a, a ? a : 16, 0)) != hipSuccess ||
+                (e = hipHostMalloc((void **)&x.h_b, b ? b : 16, 0)) != hipSuccess ||
+                (e = hipHostMalloc((void **)&x.h_c, c ? c : 16, 0)) != hipSuccess ||
+                (e = hipHostMalloc((void **)&x.h_u64, 16, 0)) != hipSuccess ||
+                (e = hipMalloc(&x.d_a, a ? a : 16)) != hipSuccess ||
+                (e = hipMalloc(&x.d_b, b ? b : 16)) != hipSuccess ||
+                (e = hipMalloc(&x.d_c, c ? c : 16)) != hipSuccess ||
+                (e = hipMalloc(&x.d_u64, 16)) != hipSuccess || (e = hipMalloc(&x.d_scr, scr)) != hipSuccess)
+                return e;
+            x.scr_bytes = scr;
+        }
+        return hipSuccess;
+    }
+};
+
+// Hand-off of finished compress chunks to the in-order writer.
+struct Ready {
+    bool done = false;
+    const uint8_t *bits = nullptr, *values = nullptr;
+    size_t nbits = 0, nvalues = 0;
+    std::atomic<bool> *released = nullptr;  // set by the writer once written
+};
+
+}  // namespace
+}  // namespace flrl
+
+using namespace flrl;
+
+extern "C" int flrl_fl_compress_file(const char *in_path, const char *out_path, int workers,
+                                     size_t chunk_bytes)
+{
+    clear_error();
+    if (!in_path || !out_path)
+        return set_error(FLRL_E_ARG, "flrl_fl_compress_file: null path");
+    int ndev = 0;
+    const int W = worker_count(workers, &ndev);
+    if (W <= 0)
+        return set_error(FLRL_E_NODEV, "flrl_fl_compress_file: no HIP device");
+    Fd in, out;
+    if ((in.fd = ::open(in_path, O_RDONLY)) < 0)
+        return set_error(FLRL_E_ARG, "[FileIO] Cannot open file: %s", in_path);
+    struct stat st;
+    if (::fstat(in.fd, &st) != 0)
+        return set_error(FLRL_E_ARG, "[FileIO] Cannot stat file: %s", in_path);
+    const uint64_t n = (uint64_t)st.st_size;
+    if ((out.fd = ::open(out_path, O_WRONLY | O_CREAT | O_TRUNC, 0644)) < 0)
+        return set_error(FLRL_E_ARG, "[FileIO] Cannot open file: %s", out_path);
+    const uint64_t F = (n + kFrame - 1) / kFrame;
+    const size_t chunk = chunk_size(chunk_bytes);
+    const size_t nchunks = n ? (size_t)((n + chunk - 1) / chunk) : 0;
+
+    Failure fail;
+    std::mutex m;
+    std::condition_variable cv;
+    std::vector<Ready> ready(nchunks);
+    const int nw = (int)(W < (int)(nchunks ? nchunks : 1) ? W : (nchunks ? nchunks : 1));
+    std::vector<std::atomic<bool>> slot_free((size_t)nw * 2);
+    for (auto &f : slot_free)
+        f.store(true);
+
+    auto worker = [&](int w) {
+        if (hipSetDevice(w % ndev) != hipSuccess) {
+            fail.set(FLRL_E_HIP, "hipSetDevice failed");
+            cv.notify_all();
+            return;
+        }
+        Slots S;
+        const size_t scr = flrl_fl_scratch_bytes(chunk);
+        if (S.alloc(chunk, chunk / kFrame, flrl_fl_values_capacity(chunk), scr) != hipSuccess) {
+            fail.set(FLRL_E_NOMEM, "Cannot allocate memory");
+            cv.notify_all();
+            return;
+        }
+        auto finish = [&](size_t c, int k) -> bool {  // stage B of chunk c in slot k
+            Slot &x = S.slot[k];
+            if (hipStreamSynchronize(x.s) != hipSuccess)
+                return false;
+            const int kerr = flrl_scratch_error(x.d_scr, x.s);
+            if (kerr) {
+                fail.set(kerr, "fl encode: device error");
+                return false;
+            }
+            const uint64_t len = (c + 1 == nchunks) ? n - (uint64_t)c * chunk : chunk;
+            const size_t fb = (size_t)((len + kFrame - 1) / kFrame);
+            const size_t vb = (size_t)x.h_u64[0];
+            if (hipMemcpyAsync(x.h_b, x.d_b, fb, hipMemcpyDeviceToHost, x.s) != hipSuccess ||
+                hipMemcpyAsync(x.h_c, x.d_c, vb, hipMemcpyDeviceToHost, x.s) != hipSuccess ||
+                hipStreamSynchronize(x.s) != hipSuccess)
+                return false;
+            std::atomic<bool> *rel = &slot_free[(size_t)w * 2 + k];
+            rel->store(false);
+            {
+                std::lock_guard<std::mutex> g(m);
+                Ready &r = ready[c];
+                r.bits = x.h_b;
+                r.nbits = fb;
+                r.values = x.h_c;
+                r.nvalues = vb;
+                r.released = rel;
+                r.done = true;
+            }
+            cv.notify_all();
+            return true;
+        };
+        size_t pend = SIZE_MAX;  // chunk waiting for stage B
+        int pend_k = 0;
+        int i = 0;
+        for (size_t c = (size_t)w; c < nchunks && !fail.failed.load(); c += (size_t)nw, ++i) {
+            const int k = i & 1;
+            Slot &x = S.slot[k];
+            {  // the writer must be done with this slot's previous chunk
+                std::unique_lock<std::mutex> g(m);
+                cv.wait(g, [&] { return slot_free[(size_t)w * 2 + k].load() || fail.failed.load(); });
+            }
+            if (fail.failed.load())
+                break;
+            const uint64_t off = (uint64_t)c * chunk;
+            const size_t len = (size_t)((c + 1 == nchunks) ? n - off : chunk);
+            if (!pread_all(in.fd, x.h_a, len, off)) {
+                fail.set(FLRL_E_ARG, "[FileIO] Cannot read file content");
+                break;
+            }
+            if (hipMemcpyAsync(x.d_a, x.h_a, len, hipMemcpyHostToDevice, x.s) != hipSuccess ||
+                flrl_fl_encode_device(x.d_a, len, x.d_b, x.d_c, x.d_u64, x.d_scr, x.scr_bytes, x.s) !=
+                    FLRL_OK ||
+                hipMemcpyAsync(x.h_u64, x.d_u64, 8, hipMemcpyDeviceToHost, x.s) != hipSuccess) {
+                fail.set(FLRL_E_HIP, std::string("fl encode: ") + flrl_last_error());
+                break;
+            }
+            if (pend != SIZE_MAX && !finish(pend, pend_k)) {
+                fail.set(FLRL_E_HIP, "fl encode: stream failed");
+                break;
+            }
+            pend = c;
+            pend_k = k;
+        }
+        if (!fail.failed.load() && pend != SIZE_MAX && !finish(pend, pend_k))
+            fail.set(FLRL_E_HIP, "fl encode: stream failed");
+        // keep the buffers alive until the writer has written them
+        std::unique_lock<std::mutex> g(m);
+        cv.wait(g, [&] {
+            return fail.failed.load() ||
+                   (slot_free[(size_t)w * 2].load() && slot_free[(size_t)w * 2 + 1].load());
+        });
+    };
+
+    std::vector<std::thread> threads;
+    for (int w = 0; w < nw && nchunks; ++w)
+        threads.emplace_back(worker, w);
+
+    // in-order writer (this thread)
+    uint64_t voff = 0;
+    for (size_t c = 0; c < nchunks; ++c) {
+        Ready r;
+        {
+            std::unique_lock<std::mutex> g(m);
+            cv.wait(g, [&] { return ready[c].done || fail.failed.load(); });
+            if (fail.failed.load())
+                break;
+            r.bits = ready[c].bits;
+            r.nbits = ready[c].nbits;
+            r.values = ready[c].values;
+            r.nvalues = ready[c].nvalues;
+            r.released = ready[c].released;
+        }
+        const uint64_t boff = kHeader + (uint64_t)c * (chunk / kFrame);
+        if (!pwrite_all(out.fd, r.bits, r.nbits, boff) ||
+            !pwrite_all(out.fd, r.values, r.nvalues, kHeader + F + voff)) {
+            fail.set(FLRL_E_ARG, "[FileIO] Cannot write to file");
+            cv.notify_all();
+            break;
+        }
+        voff += r.nvalues;
+        {
+            std::lock_guard<std::mutex> g(m);
+            r.released->store(true);
+        }
+        cv.notify_all();
+    }
+    for (auto &t : threads)
+        t.join();
+    if (fail.failed.load())
+        return set_error(fail.code ? fail.code : FLRL_E_HIP, "%s", fail.msg.c_str());
+    const uint64_t hdr[3] = {n, F, voff};
+    if (!pwrite_all(out.fd, hdr, sizeof(hdr), 0) || ::ftruncate(out.fd, (off_t)(kHeader + F + voff)) != 0)
+        return set_error(FLRL_E_ARG, "[FileIO] Cannot write to file");
+    if (::close(out.fd) != 0) {
+        out.fd = -1;
+        return set_error(FLRL_E_ARG, "[FileIO] Cannot write to file");
+    }
+    out.fd = -1;
+    return FLRL_OK;
+}
+
+extern "C" int flrl_fl_decompress_file(const char *in_path, const char *out_path, int workers,
+                                       size_t chunk_bytes)
+{
+    clear_error();
+    if (!in_path || !out_path)
+        return set_error(FLRL_E_ARG, "flrl_fl_decompress_file: null path");
+    int ndev = 0;
+    const int W = worker_count(workers, &ndev);
+    if (W <= 0)
+        return set_error(FLRL_E_NODEV, "flrl_fl_decompress_file: no HIP device");
+    Fd in, out;
+    if ((in.fd = ::open(in_path, O_RDONLY)) < 0)
+        return set_error(FLRL_E_ARG, "[FileIO] Cannot open file: %s", in_path);
+    struct stat st;
+    if (::fstat(in.fd, &st) != 0)
+        return set_error(FLRL_E_ARG, "[FileIO] Cannot stat file: %s", in_path);
+    const uint64_t fsize = (uint64_t)st.st_size;
+    uint64_t hdr[3];
+    if (fsize < kHeader || !pread_all(in.fd, hdr, sizeof(hdr), 0))
+        return set_error(FLRL_E_FORMAT, "[FileIO] truncated FL header");
+    const uint64_t n = hdr[0], F = hdr[1], V = hdr[2];
+    // format hardening: header invariants before any allocation
+    if (F != (n + kFrame - 1) / kFrame || F > fsize || V > fsize || kHeader + F + V != fsize)
+        return set_error(FLRL_E_FORMAT,
+                         "[FileIO] inconsistent FL header (inputSize %llu, bitsSize %llu, valuesSize %llu, "
+                         "file %llu bytes)",
+                         (unsigned long long)n, (unsigned long long)F, (unsigned long long)V,
+                         (unsigned long long)fsize);
+    if ((out.fd = ::open(out_path, O_WRONLY | O_CREAT | O_TRUNC, 0644)) < 0)
+        return set_error(FLRL_E_ARG, "[FileIO] Cannot open file: %s", out_path);
+    if (n == 0 || V == 0) {  // the reference's early-out: empty result (fl_cpu.cu:94-97)
+        if (::close(out.fd) != 0) {
+            out.fd = -1;
+            return set_error(FLRL_E_ARG, "[FileIO] Cannot write to file");
+        }
+        out.fd = -1;
+        return FLRL_OK;
+    }
+    const size_t chunk = chunk_size(chunk_bytes);
+    const size_t cf = chunk / kFrame;  // frames per chunk
+    const size_t nchunks = (size_t)((n + chunk - 1) / chunk);
+    // widths once; value offset of every chunk = 16 x (widths of all earlier frames)
+    std::vector<uint8_t> bits((size_t)F);
+    if (!pread_all(in.fd, bits.data(), (size_t)F, kHeader))
+        return set_error(FLRL_E_ARG, "[FileIO] Cannot read file content");
+    std::vector<uint64_t> voff(nchunks + 1);
+    {
+        uint64_t acc = 0;
+        for (size_t c = 0; c < nchunks; ++c) {
+            voff[c] = acc;
+            const size_t f1 = (c + 1) * cf < F ? (c + 1) * cf : (size_t)F;
+            uint64_t s = 0;
+            for (size_t f = c * cf; f < f1; ++f) {
+                const uint8_t b = bits[f];
+                if (b < 1 || b > 8)
+                    return set_error(FLRL_E_FORMAT, "invalid frame width %u at frame %zu", b, f);
+                s += b;
+            }
+            acc += 16 * s;
+        }
+        voff[nchunks] = V;
+        if (voff[nchunks - 1] > V)
+            return set_error(FLRL_E_FORMAT, "valuesSize %llu smaller than the widths imply",
+                             (unsigned long long)V);
+    }
+    if (::ftruncate(out.fd, (off_t)n) != 0)
+        return set_error(FLRL_E_ARG, "[FileIO] Cannot write to file");
+
+    Failure fail;
+    const int nw = (int)(W < (int)nchunks ? W : (int)nchunks);
+    auto worker = [&](int w) {
+        if (hipSetDevice(w % ndev) != hipSuccess) {
+            fail.set(FLRL_E_HIP, "hipSetDevice failed");
+            return;
+        }
+        Slots S;
+        const size_t vcap = flrl_fl_values_capacity(chunk);
+        if (S.alloc(cf, vcap, chunk, flrl_fl_scratch_bytes(chunk)) != hipSuccess) {
+            fail.set(FLRL_E_NOMEM, "Cannot allocate memory");
+            return;
+        }
+        auto finish = [&](size_t c, int k) -> bool {  // wait, check, write chunk c
+            Slot &x = S.slot[k];
+            if (hipStreamSynchronize(x.s) != hipSuccess)
+                return false;
+            const int kerr = flrl_scratch_error(x.d_scr, x.s);
+            if (kerr) {
+                fail.set(kerr, "fl decode: malformed data (widths or valuesSize)");
+                return false;
+            }
+            const uint64_t off = (uint64_t)c * chunk;
+            const size_t len = (size_t)((c + 1 == nchunks) ? n - off : chunk);
+            if (!pwrite_all(out.fd, x.h_c, len, off)) {
+                fail.set(FLRL_E_ARG, "[FileIO] Cannot write to file");
+                return false;
+            }
+            return true;
+        };
+        size_t pend = SIZE_MAX;
+        int pend_k = 0;
+        int i = 0;
+        for (size_t c = (size_t)w; c < nchunks && !fail.failed.load(); c += (size_t)nw, ++i) {
+            const int k = i & 1;
+            Slot &x = S.slot[k];
+            // slot k last held chunk c - 2*nw, finished (written) in the previous iteration
+            const uint64_t off = (uint64_t)c * chunk;
+            const size_t len = (size_t)((c + 1 == nchunks) ? n - off : chunk);
+            const size_t fb = (len + kFrame - 1) / kFrame;
+            const uint64_t vo = voff[c], vb = voff[c + 1] - voff[c];
+            if (vb > vcap) {
+                fail.set(FLRL_E_FORMAT, "valuesSize larger than the widths imply");
+                break;
+            }
+            memcpy(x.h_a, bits.data() + c * cf, fb);
+            if (!pread_all(in.fd, x.h_b, (size_t)vb, kHeader + F + vo)) {
+                fail.set(FLRL_E_ARG, "[FileIO] Cannot read file content");
+                break;
+            }
+            if (hipMemcpyAsync(x.d_a, x.h_a, fb, hipMemcpyHostToDevice, x.s) != hipSuccess ||
+                hipMemcpyAsync(x.d_b, x.h_b, (size_t)vb, hipMemcpyHostToDevice, x.s) != hipSuccess ||
+                flrl_fl_decode_device(x.d_a, fb, x.d_b, (size_t)vb, x.d_c, len, x.d_scr, x.scr_bytes, x.s) !=
+                    FLRL_OK ||
+                hipMemcpyAsync(x.h_c, x.d_c, len, hipMemcpyDeviceToHost, x.s) != hipSuccess) {
+                fail.set(FLRL_E_HIP, std::string("fl decode: ") + flrl_last_error());
+                break;
+            }
+            if (pend != SIZE_MAX && !finish(pend, pend_k))
+                break;
+            pend = c;
+            pend_k = k;
+        }
+        if (!fail.failed.load() && pend != SIZE_MAX)
+            (void)finish(pend, pend_k);
+    };
+    std::vector<std::thread> threads;
+    for (int w = 0; w < nw; ++w)
+        threads.emplace_back(worker, w);
+    for (auto &t : threads)
+        t.join();
+    if (fail.failed.load())
+        return set_error(fail.code ? fail.code : FLRL_E_HIP, "%s", fail.msg.c_str());
+    if (::close(out.fd) != 0) {
+        out.fd = -1;
+        return set_error(FLRL_E_ARG, "[FileIO] Cannot write to file");
+    }
+    out.fd = -1;
+    return FLRL_OK;
+}

@@ -4,7 +4,12 @@
 //   compress d <method> <input> <output>     decompress a file
 //
 // fl / fl-mpi / fl-nccl / fl-shmem / rl run on the GPU through the C ABI in
-// include/flrl.h (libflrl.so); fl-cpu / rl-cpu run the host codec. Errors print
+// include/flrl.h (libflrl.so); fl-cpu / rl-cpu run the host codec. The FL GPU
+// methods stream the file through the GPUs in frame-aligned chunks
+// (flrl_fl_compress_file / flrl_fl_decompress_file: `fl` one pipeline, the
+// multi-GPU methods one per GPU), so neither the file nor its output is held in
+// memory; FLRL_CHUNK_BYTES and FLRL_WORKERS override the chunk size (64 MiB)
+// and the pipeline count. Errors print
 // "[ERROR]: <message>" to stderr like the reference (main.cu:95-98), but the
 // process then exits with status 2 instead of 0, and no partial output file is
 // left behind. Phase timings print as the reference's "[TIMER]" lines.
@@ -53,8 +58,33 @@ bool is_gpu(Method m)
     return m == Method::FixedLength || m == Method::FixedLengthMulti || m == Method::RunLength;
 }
 
+size_t env_size(const char *name, size_t dflt)
+{
+    const char *v = std::getenv(name);
+    return (v && *v) ? (size_t)std::strtoull(v, nullptr, 0) : dflt;
+}
+
+// FL on the GPU(s), file to file: one call does load + encode/decode + save.
+bool fl_streamed(const Args &a, bool compress_op)
+{
+    if (a.method != Method::FixedLength && a.method != Method::FixedLengthMulti)
+        return false;
+    const int workers = (int)env_size("FLRL_WORKERS", a.method == Method::FixedLength ? 1 : 0);
+    const size_t chunk = env_size("FLRL_CHUNK_BYTES", 0);
+    Timer t;
+    if (compress_op)
+        check(flrl_fl_compress_file(a.inputFile, a.outputFile, workers, chunk), "fl compress");
+    else
+        check(flrl_fl_decompress_file(a.inputFile, a.outputFile, workers, chunk), "fl decompress");
+    t.done(compress_op ? "Compression (streamed: load + encode + save)"
+                       : "Decompression (streamed: load + decode + save)");
+    return true;
+}
+
 void compress(const Args &a)
 {
+    if (fl_streamed(a, true))
+        return;
     Timer t;
     FileData in = loadFile(a.inputFile);
     t.done("Load data from file");
@@ -110,6 +140,8 @@ void compress(const Args &a)
 
 void decompress(const Args &a)
 {
+    if (fl_streamed(a, false))
+        return;
     Timer t;
     FileData out;
     const bool rl = a.method == Method::RunLength || a.method == Method::RunLengthCPU;

@@ -89,6 +89,21 @@ int flrl_fl_decompress(size_t output_size, const uint8_t *bits, size_t bits_size
  * result is byte-identical to flrl_fl_compress. */
 int flrl_fl_compress_sharded(const uint8_t *data, size_t size, int ngpus, flrl_fl_buf *out);
 
+/* ---- FL, file to file, streamed through GPUs ---
+ * The CLI's `c|d fl` (workers = 1) and `fl-mpi` / `fl-nccl` / `fl-shmem`
+ * (workers <= 0: one per visible GPU) paths; replaces main.cu:81-117 (load,
+ * encode, save) and :139-161 without holding the file in memory: frame-aligned
+ * chunks of `chunk_bytes` (0: 64 MiB; rounded down to a multiple of 128) go
+ * through `workers` pipelines (worker w on device w % devices; more workers
+ * than devices is allowed), pread -> H2D -> device codec -> D2H -> pwrite, two
+ * chunks in flight per worker. Output files are byte-identical to
+ * flrl_fl_compress + the FL container (file_io.cu:222-280). Decompression
+ * validates the header (bitsSize == ceil(inputSize/128), file length ==
+ * 24 + bitsSize + valuesSize) and every width before decoding (FLRL_E_FORMAT).
+ * On error the output file may be partial; the caller removes it. */
+int flrl_fl_compress_file(const char *in_path, const char *out_path, int workers, size_t chunk_bytes);
+int flrl_fl_decompress_file(const char *in_path, const char *out_path, int workers, size_t chunk_bytes);
+
 /* ---- FL, device-resident (asynchronous on `stream`) -----------------------
  * Replaces FixedLength::gpuCompressDevice (src/fl/fl_gpu.cuh:17,
  * fl_gpu.cu:425-535) — outputs stay in HBM.

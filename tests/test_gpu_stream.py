@@ -1,0 +1,154 @@
+"""Streamed FL file codec (flrl_fl_compress_file / flrl_fl_decompress_file, the
+CLI's GPU FL path) against the oracle.
+
+Frame-aligned chunks through several pipelines must give the same file as the
+whole-input oracle encode (the concatenation identity):
+chunk sizes from one frame up, more workers than GPUs (so the multi-worker
+ordering logic runs on a 1-GPU box), ragged tails, the empty file, and the
+reference's BMP through the CLI. Decompression must reject malformed files."""
+import hashlib
+import os
+import struct
+import subprocess
+
+import numpy as np
+import pytest
+
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+flrl = pytest.importorskip("flrl")
+
+
+def _oracle_file(data: np.ndarray) -> bytes:
+    return oracle.fl_file_bytes(data)
+
+
+def _input(kind: str, n: int, seed: int = 7) -> np.ndarray:
+    if kind == "mixed":
+        a = oracle.gen("lo4", n, seed)
+        a[::997] = 0xE1  # every width appears
+        a[5000:9000] = 0
+        return a
+    return oracle.gen(kind, n, seed)
+
+
+@pytest.mark.parametrize("n", [1, 127, 128, 129, 4096 * 3 + 17, (5 << 20) + 77])
+@pytest.mark.parametrize("chunk,workers", [(128, 1), (4096, 3), (1 << 20, 2), (0, 1)])
+def test_compress_file_matches_oracle(tmp_path, n, chunk, workers):
+    if chunk == 128 and n > 100_000:
+        pytest.skip("one-frame chunks: small inputs only (one H2D per 128 bytes)")
+    data = _input("mixed", n)
+    src, dst, back = tmp_path / "in", tmp_path / "out.fl", tmp_path / "back"
+    data.tofile(src)
+    flrl.fl_compress_file(str(src), str(dst), workers, chunk)
+    assert dst.read_bytes() == _oracle_file(data)
+    flrl.fl_decompress_file(str(dst), str(back), workers, chunk)
+    assert back.read_bytes() == data.tobytes()
+
+
+@pytest.mark.parametrize("kind", ["u8", "lo4", "runs32", "zero"])
+def test_file_round_trip_kinds(tmp_path, kind):
+    n = (24 << 20) + 333
+    data = _input(kind, n, 11)
+    src, dst, back = tmp_path / "in", tmp_path / "out.fl", tmp_path / "back"
+    data.tofile(src)
+    flrl.fl_compress_file(str(src), str(dst), 4, 5 << 20)
+    assert hashlib.sha256(dst.read_bytes()).hexdigest() == hashlib.sha256(_oracle_file(data)).hexdigest()
+    flrl.fl_decompress_file(str(dst), str(back), 3, 3 << 20)
+    assert back.read_bytes() == data.tobytes()
+
+
+def test_empty_file(tmp_path):
+    src, dst, back = tmp_path / "in", tmp_path / "out.fl", tmp_path / "back"
+    src.write_bytes(b"")
+    flrl.fl_compress_file(str(src), str(dst), 2, 0)
+    assert dst.read_bytes() == bytes(24)  # empty input -> 24 zero bytes
+    flrl.fl_decompress_file(str(dst), str(back), 2, 0)
+    assert back.read_bytes() == b""
+
+
+def test_decode_chunking_independent_of_encode(tmp_path):
+    data = _input("mixed", (3 << 20) + 5, 3)
+    src, dst = tmp_path / "in", tmp_path / "out.fl"
+    data.tofile(src)
+    flrl.fl_compress_file(str(src), str(dst), 1, 1 << 20)
+    for chunk, workers in ((128 * 7, 2), (1 << 16, 5), (0, 1)):
+        back = tmp_path / f"back{chunk}"
+        flrl.fl_decompress_file(str(dst), str(back), workers, chunk)
+        assert back.read_bytes() == data.tobytes()
+
+
+def _bad(tmp_path, blob: bytes, name: str):
+    p = tmp_path / name
+    p.write_bytes(blob)
+    with pytest.raises(flrl.FLRLError) as e:
+        flrl.fl_decompress_file(str(p), str(tmp_path / (name + ".out")), 2, 4096)
+    return e.value
+
+
+def test_malformed_files_rejected(tmp_path):
+    data = _input("mixed", 10_000, 5)
+    good = _oracle_file(data)
+    n, F, V = struct.unpack_from("<QQQ", good)
+    body = good[24:]
+    assert _bad(tmp_path, good[:20], "short").code == 4
+    assert _bad(tmp_path, struct.pack("<QQQ", n, F + 1, V) + body, "bits").code == 4
+    assert _bad(tmp_path, struct.pack("<QQQ", n, F, V + 1) + body, "vals").code == 4
+    assert _bad(tmp_path, good[:-1], "trunc").code == 4
+    for w in (0, 9):
+        b = bytearray(good)
+        b[24 + 3] = w
+        assert _bad(tmp_path, bytes(b), f"w{w}").code == 4
+    # widths consistent with F but values one frame short: sizes disagree
+    b = bytearray(good)
+    b[24] = b[24] + 1 if b[24] < 8 else b[24] - 1
+    assert _bad(tmp_path, bytes(b), "sum").code == 4
+
+
+def test_missing_input(tmp_path):
+    with pytest.raises(flrl.FLRLError):
+        flrl.fl_compress_file(str(tmp_path / "nope"), str(tmp_path / "o"), 1, 0)
+
+
+def test_cli_streamed_bmp(golden, bmp_bytes, cli_path, tmp_path):
+    src = tmp_path / "in.bmp"
+    src.write_bytes(bmp_bytes)
+    env = dict(os.environ, FLRL_CHUNK_BYTES=str(128 * 1000), FLRL_WORKERS="3")
+    for method in ("fl", "fl-nccl"):
+        out, back = tmp_path / f"{method}.fl", tmp_path / f"{method}.bmp"
+        r = subprocess.run([cli_path, "c", method, str(src), str(out)], env=env,
+                           capture_output=True, text=True)
+        assert r.returncode == 0, r.stderr
+        assert "[TIMER]" in r.stdout
+        assert hashlib.sha256(out.read_bytes()).hexdigest() == golden["fl_bmp"]["fl_sha256"]
+        r = subprocess.run([cli_path, "d", method, str(out), str(back)], env=env,
+                           capture_output=True, text=True)
+        assert r.returncode == 0, r.stderr
+        assert back.read_bytes() == bmp_bytes
+
+
+def test_cli_streamed_error_removes_output(cli_path, tmp_path):
+    bad = tmp_path / "bad.fl"
+    bad.write_bytes(struct.pack("<QQQ", 1000, 3, 5) + bytes(8))
+    out = tmp_path / "out"
+    r = subprocess.run([cli_path, "d", "fl", str(bad), str(out)], capture_output=True, text=True)
+    assert r.returncode == 2 and "[ERROR]" in r.stderr
+    assert not out.exists()
+
+
+def test_large_file_default_chunks(tmp_path):
+    n = (300 << 20) + 4097  # 5 default 64 MiB chunks, ragged tail
+    data = oracle.gen("u8", n, 42)
+    src, dst, back = tmp_path / "in", tmp_path / "out.fl", tmp_path / "back"
+    data.tofile(src)
+    flrl.fl_compress_file(str(src), str(dst), 0, 0)
+    bits, values = oracle.fl_compress(data)
+    blob = dst.read_bytes()
+    assert blob[:24] == struct.pack("<QQQ", n, bits.size, values.size)
+    assert blob[24:24 + bits.size] == bits.tobytes()
+    assert blob[24 + bits.size:] == values.tobytes()
+    del blob
+    flrl.fl_decompress_file(str(dst), str(back), 2, 0)
+    assert back.read_bytes() == data.tobytes()
