@@ -310,6 +310,9 @@ __global__ __launch_bounds__(T) void rl_encode_kernel(
     uint8_t *const img = s_lds;
     uint8_t *const stc = s_lds + TB + (size_t)(threadIdx.x / kWave) * 2 * SW;
     uint8_t *const stv = stc + SW;
+    constexpr int SC = kRlStageBytes / 2;  // tile staging: runs
+    uint8_t *const tsc = s_lds + TB;        // counts[SC] | values[SC] (same bytes as the per-wave areas)
+    uint8_t *const tsv = tsc + SC;
     uint32_t *const s_wmap = reinterpret_cast<uint32_t *>(s_lds + TB + kRlStageBytes);
     uint32_t *const s_wfirst = s_wmap + W;
     uint32_t *const s_wh = s_wfirst + W;
@@ -438,20 +441,93 @@ __global__ __launch_bounds__(T) void rl_encode_kernel(
     const uint64_t tmap = K ? sm_nat(tile_first, K, tile_map & 0xFFu) : sm_nonat(tile_len);
     FLRL_RL_PHASE(1);
 
+    // ---- stage the runs that do not depend on the incoming state (all heads
+    // from the tile's first natural head on) at their tile-local index, while
+    // wave 0 resolves the look-back: waves 1.. stage first, wave 0 after
+    const bool staged = K <= (uint32_t)SC;  // tile-uniform
+    auto stage_lane = [&]() {
+        if (!K || o + LB <= tile_first)
+            return;  // no state-independent head in this lane
+        const bool after = o > tile_first;  // else: the lane holding the first natural head
+        const uint32_t cr = after ? pm_apply(lane_rel, 1) : 0u;  // constant after it
+        const uint32_t j0 = cr == 0 ? 0u : 255u - cr;
+        const bool split = after && j0 < fpos && j0 < vbl;
+        uint64_t h0 = 0, h1 = 0;
+#pragma unroll
+        for (int c = 0; c < CH; ++c) {
+            uint32_t h = (nat[c / 2] >> (16 * (c & 1))) & 0xFFFFu;
+            if (split && (j0 >> 4) == (uint32_t)c)
+                h |= 1u << (j0 & 15u);
+            if (c < 4)
+                h0 |= (uint64_t)h << (16 * c);
+            else
+                h1 |= (uint64_t)h << (16 * (c - 4));
+        }
+        uint32_t slot = wave_hbase + (hincl - indep);
+        int prev = -1;
+        while (h0 | h1) {
+            int pos;
+            if (h0) {
+                pos = __builtin_ctzll(h0);
+                h0 &= h0 - 1;
+            } else {
+                pos = 64 + __builtin_ctzll(h1);
+                h1 &= h1 - 1;
+            }
+            // the tile's first record (the first natural head) gets its count later
+            uint32_t cnt = prev < 0 ? add_c(cr, (uint32_t)pos) : (uint32_t)(pos - prev);
+            cnt = cnt == 0 ? 255u : cnt;
+            const uint32_t q = (uint32_t)pos - 1;
+            const uint32_t val = pos == 0 ? p0 : my[(((q >> 4) ^ (row & 7u)) * 16) + (q & 15u)];
+            tsc[slot] = (uint8_t)cnt;
+            tsv[slot] = (uint8_t)val;
+            ++slot;
+            prev = pos;
+        }
+    };
+    if (staged && w != 0)
+        stage_lane();
+
     // ---- one look-back: (heads before the tile, chunk state at its start) --
     if (w == 0) {
         publish_seg(status, tile, tmap);
         const uint64_t state = lookback_seg<kRlLookG>(status, tile, tmap, ctrl);
         if (lane == 0)
             *s_state = state;
+        if (staged)
+            stage_lane();
     }
     __syncthreads();
     FLRL_RL_PHASE(2);
     const uint64_t h_in = sm_h(*s_state);
     const uint32_t c_in = sm_c(*s_state);
+    const uint32_t S = splits(c_in, pre);  // split heads before the first natural head
+    if (staged) {
+        // split heads h_in + s end full 255-byte chunks of the tile's first byte
+        const uint8_t v0 = img[0];
+        for (uint32_t j = (uint32_t)tid; j < S; j += T) {
+            const uint64_t gi = h_in + j;
+            if (gi > 0) {
+                counts[gi - 1] = 255;
+                values[gi - 1] = v0;
+            }
+        }
+        const uint64_t g0 = h_in + S;  // global index of the first natural head
+        if (K) {
+            if (tid == 0 && g0 > 0) {
+                const uint32_t c = add_c(c_in, tile_first);
+                counts[g0 - 1] = (uint8_t)(c == 0 ? 255u : c);
+                values[g0 - 1] = tsv[0];
+            }
+            for (uint32_t j = 1 + (uint32_t)tid; j < K; j += T) {
+                counts[g0 + j - 1] = tsc[j];
+                values[g0 + j - 1] = tsv[j];
+            }
+        }
+    } else {
+    // dense tile (more than SC state-independent runs): emit after the look-back
     const uint32_t c_lane = pm_apply(lane_rel, c_in);
-    uint64_t g = (K && o > tile_first) ? h_in + splits(c_in, pre) + wave_hbase + (hincl - indep)
-                                       : h_in + splits(c_in, o);
+    uint64_t g = (K && o > tile_first) ? h_in + S + wave_hbase + (hincl - indep) : h_in + splits(c_in, o);
 
     // ---- head masks with the true states, then the lane's runs in order -----
     uint64_t hm0 = 0, hm1 = 0;  // chunks 0-3 / 4-7
@@ -553,12 +629,13 @@ __global__ __launch_bounds__(T) void rl_encode_kernel(
             }
         }
     }
+    }
     FLRL_RL_PHASE(3);
     FLRL_RL_PHASE_END();
 
     // ---- the final run (ends at byte n-1) ----------------------------------
     if (tile + 1 == ntiles && tid == 0) {
-        const uint64_t R = h_in + splits(c_in, pre) + K;
+        const uint64_t R = h_in + S + K;
         const uint32_t c_end = pm_apply(tile_map, c_in);
         counts[R - 1] = (uint8_t)(c_end == 0 ? 255u : c_end);
         values[R - 1] = in[n - 1];
