@@ -709,8 +709,7 @@ __global__ __launch_bounds__(kThreads) void rl_offsets_kernel(
 
 // ---- decode: expand one tile of kRdRuns runs ------------------------------
 // The tile's output [base, end) is produced in kRdWindow-byte windows aligned to
-// global 16-byte boundaries: the runs overlapping a window (one binary search
-// of the count prefix per window) memset their bytes into an LDS window with
+// global 16-byte boundaries: the runs overlapping a window memset their bytes into an LDS window with
 // aligned dword stores, then the window leaves in 16-byte stores (the two
 // chunks a tile shares with its neighbours byte by byte).
 __device__ __forceinline__ uint32_t run_lower(const uint32_t *pre, uint32_t nr, uint32_t x)
@@ -735,6 +734,7 @@ __global__ __launch_bounds__(kRdThreads) void rl_decode_kernel(
     __shared__ u32x4 s_val4[kRdRuns / 16];
     __shared__ u32x4 s_win4[kRdWindow / 16];
     __shared__ uint32_t s_wave[kRdThreads / kWave];
+    __shared__ uint32_t s_next;
     uint8_t *s_val = reinterpret_cast<uint8_t *>(s_val4);
     uint8_t *s_win = reinterpret_cast<uint8_t *>(s_win4);
     uint32_t *s_win32 = reinterpret_cast<uint32_t *>(s_win4);
@@ -782,16 +782,21 @@ __global__ __launch_bounds__(kRdThreads) void rl_decode_kernel(
         s_pre[kRdRuns] = (uint32_t)(end - base);
     __syncthreads();
 
-    // ---- windows ---------------------------------------------------------------
+    // ---- windows: the first run of a window is found by one binary search per
+    // tile, later ones are handed on by the thread whose run crosses the
+    // window end; a thread stops at the first run starting past the window
     const uint64_t g0 = base & ~15ull;
+    uint32_t ja = run_lower(s_pre, nr, 0);
     for (uint64_t gw = g0; gw < end; gw += kRdWindow) {
         const uint32_t lo = (uint32_t)((gw > base ? gw : base) - base);  // owned, tile-local
         const uint32_t hi = (uint32_t)((gw + kRdWindow < end ? gw + kRdWindow : end) - base);
         const uint32_t shift = (uint32_t)(gw < base ? base - gw : 0);    // window pos of local lo
-        const uint32_t ja = run_lower(s_pre, nr, lo);
-        const uint32_t jb = run_lower(s_pre, nr, hi - 1) + 1;
-        for (uint32_t j = ja + tid; j < jb; j += kRdThreads) {
-            uint32_t x = s_pre[j], y = j + 1 < nr ? s_pre[j + 1] : hi;
+        for (uint32_t j = ja + tid; j < nr && s_pre[j] < hi; j += kRdThreads) {
+            uint32_t x = s_pre[j], y = s_pre[j + 1];  // s_pre[nr] = the tile's total
+            if (y > hi)
+                s_next = j;  // crosses into the next window (exactly one run)
+            else if (y == hi)
+                s_next = j + 1;
             x = x < lo ? lo : x;
             y = y > hi ? hi : y;
             if (x >= y)
@@ -808,6 +813,7 @@ __global__ __launch_bounds__(kRdThreads) void rl_decode_kernel(
             while (p < q) s_win[p++] = (uint8_t)v;
         }
         __syncthreads();
+        ja = s_next;
         const uint32_t wlen = (uint32_t)(end - gw < (uint64_t)kRdWindow ? end - gw : kRdWindow);
         for (uint32_t ch = tid; ch * 16 < wlen; ch += kRdThreads) {
             const uint64_t gp = gw + 16ull * ch;

@@ -7,6 +7,7 @@
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
+#include <string.h>
 
 __device__ unsigned long long g_ph[64];
 __device__ __forceinline__ uint64_t rl_stamp()
@@ -100,6 +101,37 @@ int main(int argc, char **argv)
     printf("rl_encode kind %d n %zu runs %llu: avg %.4f ms best %.4f ms (%.1f GB/s alg avg)  err %d\n", kind, n,
            (unsigned long long)runs, sum / reps, best, (n + 2.0 * runs) / (sum / reps) / 1e6,
            flrl_scratch_error(d_scr, nullptr));
+    {  // decode of what was just encoded, checked against the input
+        uint8_t *d_out;
+        CK(hipMalloc(&d_out, n + 64));
+        const size_t dscr = flrl_rl_decode_scratch_bytes(runs);
+        void *d_dscr;
+        CK(hipMalloc(&d_dscr, dscr));
+        float dsum = 0, dbest = 1e30f;
+        for (int r = 0; r < reps + 3; ++r) {
+            CK(hipEventRecord(e0, nullptr));
+            if (flrl_rl_decode_device(d_c, d_v, runs, d_out, n, d_dscr, dscr, nullptr) != FLRL_OK) {
+                fprintf(stderr, "decode: %s\n", flrl_last_error());
+                return 1;
+            }
+            CK(hipEventRecord(e1, nullptr));
+            CK(hipEventSynchronize(e1));
+            float ms;
+            CK(hipEventElapsedTime(&ms, e0, e1));
+            if (r >= 3) {
+                dsum += ms;
+                dbest = ms < dbest ? ms : dbest;
+            }
+        }
+        uint8_t *h_a = (uint8_t *)malloc(n), *h_b = (uint8_t *)malloc(n);
+        CK(hipMemcpy(h_a, d_in, n, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(h_b, d_out, n, hipMemcpyDeviceToHost));
+        printf("rl_decode: avg %.4f ms best %.4f ms (%.1f GB/s alg avg)  err %d  roundtrip %s\n", dsum / reps, dbest,
+               (n + 2.0 * runs) / (dsum / reps) / 1e6, flrl_scratch_error(d_dscr, nullptr),
+               memcmp(h_a, h_b, n) == 0 ? "ok" : "MISMATCH");
+        free(h_a);
+        free(h_b);
+    }
 #ifdef STAMP
     unsigned long long ph[64];
     CK(hipMemcpyFromSymbol(ph, HIP_SYMBOL(g_ph), sizeof(ph)));
