@@ -97,6 +97,18 @@ def cpu_baseline(kind: str, seed: int, sample: int, gpu_bits, gpu_values):
     }
 
 
+def workload_ref(n: int, kind: str, world: int) -> str:
+    """Which BASELINE.json config (or north-star target) this FL workload is."""
+    if kind == "u8" and n == 1 << 30:
+        return "BASELINE configs[1]" + (f", weak-scaled x{world}" if world > 1 else "")
+    if kind == "lo4" and n == 16 << 30 and world == 1:
+        return "BASELINE configs[3]"
+    if kind == "u8" and n == 16 << 30:
+        return ("north-star target: 16 GiB uniform-random at 1 GPU" if world == 1
+                else f"BASELINE configs[4]: 16 GiB per GPU x{world}")
+    return "custom size"
+
+
 def rl_section(n: int, seed: int, steps: int, warmup: int, dev, cpu: bool):
     """BASELINE configs[2]: RL encode/decode of n bytes of runs32 (mean run 32).
     Input generated on the host by the product generator (runs32 is
@@ -284,7 +296,7 @@ def main():
             "dtype": "u8",
             "data": f"synthetic ({args.kind} splitmix64 seed {args.seed}, SURVEY.md §8(d), generated in HBM)",
             "config": {
-                "workload": f"FL encode+decode of {n} {args.kind} bytes per GPU (BASELINE configs[1] at 1 GiB)",
+                "workload": f"FL encode+decode of {n} {args.kind} bytes per GPU ({workload_ref(n, args.kind, world)})",
                 "bytes_per_gpu": n,
                 "global_bytes": n * world,
                 "parallelism": f"dp{world}: 128-aligned shards, RCCL size-scan" if world > 1 else "single GPU",
