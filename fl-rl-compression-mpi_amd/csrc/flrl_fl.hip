@@ -199,11 +199,13 @@ __global__ __launch_bounds__(T, 1) void fl_encode_kernel(
         FLRL_FL_TRACE(tile, 1);
 
         // ---- bits[] for this tile's frames
+        // (not by wave 0: its look-back status loads would queue behind these
+        // stores, vmcnt being in order)
         if (frame0 + TF <= nframes) {
-            for (int i = tid; i < TF / 16; i += T)
+            for (int i = tid - kWave; i >= 0 && i < TF / 16; i += T - kWave)
                 reinterpret_cast<u32x4 *>(bits + frame0)[i] = s_w4[i];
         } else {
-            for (int i = tid; i < TF; i += T)
+            for (int i = tid - kWave; i >= 0 && i < TF; i += T - kWave)
                 if (frame0 + i < nframes)
                     bits[frame0 + i] = s_w[i];
         }
