@@ -166,7 +166,9 @@ __global__ __launch_bounds__(T, 1) void fl_encode_kernel(
     load_tile<T, ITEMS>(a, in, (uint64_t)tile * TB, n);
 
     for (;;) {
-        __syncthreads();  // previous tile's LDS readers are done; s_next consumed
+        // no barrier here: s_out/s_w of the previous tile are re-written only
+        // after the widths barrier below, which every wave reaches after its
+        // stores; s_next was read by all before the previous look-back barrier
         if (tid == 0)
             s_next = atomicAdd(&ctrl->ticket, 1u);  // next ticket, read after the barrier below
         FLRL_FL_TRACE(tile, 0);
