@@ -78,21 +78,25 @@ __device__ __forceinline__ uint64_t unpack8(uint64_t w, uint32_t b)
 
 __device__ __forceinline__ uint32_t clamp_width(uint32_t b) { return b < 1 ? 1u : (b > 8 ? 8u : b); }
 
+// Encode tile layout: lane group g = tid/8 owns ITEMS consecutive frames
+// g*ITEMS .. +ITEMS-1; item k of lane tid is 16-byte chunk tid%8 of frame
+// g*ITEMS + k. A load instruction thus fetches T/8 full 128-byte frames.
 template <int T, int ITEMS>
-__device__ __forceinline__ void load_tile(u32x4 (&v)[ITEMS], const uint8_t *in, uint64_t off,
-                                          uint64_t n)
+__device__ __forceinline__ void load_tile_g(u32x4 (&v)[ITEMS], const uint8_t *in, uint64_t off,
+                                            uint64_t n)
 {
     constexpr int TB = T * 16 * ITEMS;
     const int tid = threadIdx.x;
+    const uint32_t lo = (uint32_t)(tid >> 3) * ITEMS * kFrame + (uint32_t)(tid & 7) * 16;
     if (off + TB <= n) {
-        const u32x4 *src = reinterpret_cast<const u32x4 *>(in + off);
+        const uint8_t *src = in + off + lo;
 #pragma unroll
         for (int k = 0; k < ITEMS; ++k)
-            v[k] = __builtin_nontemporal_load(src + k * T + tid);
+            v[k] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(src + k * kFrame));
     } else {
 #pragma unroll
         for (int k = 0; k < ITEMS; ++k)
-            v[k] = load16_tail(in, off + (uint64_t)(k * T + tid) * 16, n);
+            v[k] = load16_tail(in, off + lo + (uint64_t)k * kFrame, n);
     }
 }
 
@@ -126,9 +130,12 @@ __device__ __forceinline__ void stage_packed(uint8_t *s, uint32_t off, uint32_t 
 
 // FL encode: persistent, one T-thread workgroup per CU, 16*T*ITEMS-byte tiles
 // (128 KiB at T = 512, ITEMS = 16) taken by ticket. Per tile: widths (OR of
-// each frame's 8 lanes), LDS scan, publish the width sum, pack into the LDS
-// staging tile, prefetch the next tile into the freed registers, resolve the
-// tile's offset by look-back (wave 0), stream the staged bytes out. Wave 0
+// each frame's 8 lanes); a lane group's 16 frames are consecutive, so frame
+// offsets are a register running sum after one wave scan of group totals and
+// one LDS exchange of wave totals (2 barriers per tile in all); publish the
+// width sum, pack into the LDS staging tile, prefetch the next tile into the
+// freed registers, resolve the tile's offset by look-back (wave 0), stream the
+// staged bytes out. Wave 0
 // issues its share of the prefetch only after its look-back: vmcnt is per wave
 // and in order, so status loads issued behind 16 bulk loads would each wait
 // for all of them (measured: scripts/ubench_encode.hip).
@@ -147,10 +154,10 @@ __global__ __launch_bounds__(T, 1) void fl_encode_kernel(
     constexpr int TF = TB / kFrame;
     __shared__ u32x4 s_out[TB / 16];
     __shared__ u32x4 s_w4[TF / 16];
-    __shared__ uint32_t s_pref[TF];
     __shared__ uint32_t s_wave[T / kWave];
     __shared__ uint32_t s_next;
     __shared__ uint64_t s_base;
+    static_assert(ITEMS == 16, "a lane group's 16 frame widths are one 16-byte vector");
     uint8_t *s_w = reinterpret_cast<uint8_t *>(s_w4);
     uint8_t *s_out_b = reinterpret_cast<uint8_t *>(s_out);
 
@@ -163,7 +170,7 @@ __global__ __launch_bounds__(T, 1) void fl_encode_kernel(
     if (tile >= ntiles)
         return;
     u32x4 a[ITEMS];
-    load_tile<T, ITEMS>(a, in, (uint64_t)tile * TB, n);
+    load_tile_g<T, ITEMS>(a, in, (uint64_t)tile * TB, n);
 
     for (;;) {
         // no barrier here: s_out/s_w of the previous tile are re-written only
@@ -175,7 +182,11 @@ __global__ __launch_bounds__(T, 1) void fl_encode_kernel(
         const uint64_t frame0 = (uint64_t)tile * TF;
 
         // ---- frame widths: OR over the frame's 8 lanes, b = max(1, bitlen)
+        // and the scan: a lane group's frames are consecutive, so its prefix is a
+        // register running sum; groups scan across the wave, waves through LDS
         uint32_t bw[ITEMS];
+        uint32_t gtot = 0;
+        u32x4 wv = u32x4{0u, 0u, 0u, 0u};
 #pragma unroll
         for (int k = 0; k < ITEMS; ++k) {
             uint32_t o = a[k].x | a[k].y | a[k].z | a[k].w;
@@ -183,17 +194,28 @@ __global__ __launch_bounds__(T, 1) void fl_encode_kernel(
             o |= o >> 8;
             o = or_8lanes(o & 0xFFu);
             uint32_t b = o ? 32u - __clz(o) : 1u;
-            const int ft = k * (T / 8) + (tid >> 3);
+            const int ft = (tid >> 3) * ITEMS + k;
             if (frame0 + ft >= nframes)
                 b = 0;  // past the last frame: contributes nothing
             bw[k] = b;
-            if ((tid & 7) == 0)
-                s_w[ft] = (uint8_t)b;
+            gtot += b;
+            wv[k >> 2] |= b << (8 * (k & 3));
         }
+        const int lane = tid & (kWave - 1);
+        const uint32_t gincl = wave_incl_scan_u32((lane & 7) == 0 ? gtot : 0u);
+        if (lane == kWave - 1)
+            s_wave[wave] = gincl;
+        if ((tid & 7) == 0)
+            s_w4[tid >> 3] = wv;
         __syncthreads();
         const uint32_t nxt = s_next;
-        const uint32_t agg = block_excl_scan<TF, uint8_t, T>(s_w, s_pref, s_wave);
-        __syncthreads();
+        uint32_t wbase = 0, agg = 0;
+#pragma unroll
+        for (int v = 0; v < T / kWave; ++v) {
+            const uint32_t t = s_wave[v];
+            wbase += v < wave ? t : 0u;
+            agg += t;
+        }
 
         // ---- publish the tile's width sum early (successors' look-backs need it)
         if (tid == 0)
@@ -213,13 +235,14 @@ __global__ __launch_bounds__(T, 1) void fl_encode_kernel(
         }
 
         // ---- pack 16 values -> 2b bytes per lane into the LDS staging tile
+        uint32_t run = wbase + gincl - gtot;  // widths before this group's first frame
 #pragma unroll
         for (int k = 0; k < ITEMS; ++k) {
             const uint32_t b = bw[k];
+            const uint32_t off = 16u * run + 2u * b * (uint32_t)(tid & 7);
+            run += b;
             if (b == 0)
                 continue;
-            const int ft = k * (T / 8) + (tid >> 3);
-            const uint32_t off = 16u * s_pref[ft] + 2u * b * (uint32_t)(tid & 7);
             const uint64_t x0 = ((uint64_t)a[k].y << 32) | a[k].x;
             const uint64_t x1 = ((uint64_t)a[k].w << 32) | a[k].z;
             uint64_t lo = x0, hi = x1;
@@ -234,14 +257,14 @@ __global__ __launch_bounds__(T, 1) void fl_encode_kernel(
         // ---- prefetch the next tile into the freed registers (wave 0: later)
         const bool more = nxt < ntiles;
         if (more && wave != 0)
-            load_tile<T, ITEMS>(a, in, (uint64_t)nxt * TB, n);
+            load_tile_g<T, ITEMS>(a, in, (uint64_t)nxt * TB, n);
         if (wave == 0) {
             const uint64_t excl = lookback_resolve(status, tile, agg, ctrl);
             if (tid == 0)
                 s_base = excl;
             FLRL_FL_TRACE(tile, 2);
             if (more)
-                load_tile<T, ITEMS>(a, in, (uint64_t)nxt * TB, n);
+                load_tile_g<T, ITEMS>(a, in, (uint64_t)nxt * TB, n);
         }
         __syncthreads();
 
@@ -261,7 +284,7 @@ __global__ __launch_bounds__(T, 1) void fl_encode_kernel(
             // last tile: valuesSize = 16*(frames before last) + ceil(cnt*b_last/8)
             const int fl = (int)(nframes - 1 - frame0);
             const uint64_t cnt = n - (nframes - 1) * kFrame;
-            const uint64_t vsize = 16ull * (base + s_pref[fl]) + (cnt * s_w[fl] + 7) / 8;
+            const uint64_t vsize = 16ull * (base + agg - s_w[fl]) + (cnt * s_w[fl] + 7) / 8;
             if (tid == 0)
                 *values_size = vsize;
             for (uint32_t c = tid; c < agg; c += T)

@@ -9,6 +9,7 @@
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
+#include <string.h>
 
 #ifdef TRACE
 __device__ uint64_t *g_trace;
@@ -97,11 +98,20 @@ int main(int argc, char **argv)
             bd = ms < bd ? ms : bd;
         }
     }
+    bool rt_ok;
+    {  // round trip of the last encode/decode
+        uint8_t *h_a = (uint8_t *)malloc(n), *h_b = (uint8_t *)malloc(n);
+        CK(hipMemcpy(h_a, d_in, n, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(h_b, d_out, n, hipMemcpyDeviceToHost));
+        rt_ok = memcmp(h_a, h_b, n) == 0;
+        free(h_a);
+        free(h_b);
+    }
     const double alg = (double)n + F + vs;
     printf("fl kind %d n %zu V %llu: encode avg %.4f best %.4f ms (%.1f GB/s alg)  decode avg %.4f best %.4f ms "
-           "(%.1f GB/s alg)  err %d\n",
+           "(%.1f GB/s alg)  err %d  roundtrip %s\n",
            kind, n, (unsigned long long)vs, se / reps, be, alg / (se / reps) / 1e6, sd / reps, bd,
-           alg / (sd / reps) / 1e6, flrl_scratch_error(d_scr, nullptr));
+           alg / (sd / reps) / 1e6, flrl_scratch_error(d_scr, nullptr), rt_ok ? "ok" : "MISMATCH");
 #ifdef TRACE
     CK(hipMemset(d_tr, 0, ntiles * 32));
     flrl_fl_encode_device(d_in, n, d_bits, d_vals, d_vs, d_scr, scr, nullptr);
