@@ -20,6 +20,7 @@ from __future__ import annotations
 
 import argparse
 import hashlib
+import struct
 import json
 import os
 import sys
@@ -53,6 +54,8 @@ def parse():
     p.add_argument("--cpu-sample", type=int, default=-1,
                    help="bytes of the workload the CPU oracle times (default: min(bytes, 1 GiB)); 0 = skip")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"))
+    p.add_argument("--no-north-star", action="store_true",
+                   help="skip the 16 GiB u8 FL encode (BASELINE north-star target) at N=1")
     p.add_argument("--no-rl", action="store_true",
                    help="skip the RL section (config #3: 1 GiB runs32), which runs at N=1 only")
     return p.parse_args()
@@ -107,6 +110,61 @@ def workload_ref(n: int, kind: str, world: int) -> str:
         return ("north-star target: 16 GiB uniform-random at 1 GPU" if world == 1
                 else f"BASELINE configs[4]: 16 GiB per GPU x{world}")
     return "custom size"
+
+
+def north_star_section(seed: int, steps: int, warmup: int, dev):
+    """BASELINE north star: FL encode of 16 GiB uniform-random bytes on 1 GPU,
+    target >= 70 % of HBM peak on algorithmic bytes. Encode and
+    decode timed with HIP events; parity: device round trip, and the first
+    1 GiB of the output (frame-aligned, so byte-identical to a 1 GiB encode,
+    SURVEY.md fact 7) hashes to the reference fl-cpu's 1 GiB file."""
+    n = 16 << 30
+    x = gen("u8", n, seed, word_offset=0, device=dev)
+    codec = FLDevice(n, dev)
+    stream = torch.cuda.current_stream()
+    for _ in range(max(1, warmup)):
+        codec.encode(x)
+    v = codec.values_size()
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(2)] for _ in range(steps)]
+    torch.cuda.synchronize()
+    for k in range(steps):
+        ev[k][0].record(stream)
+        codec.encode(x)
+        ev[k][1].record(stream)
+    torch.cuda.synchronize()
+    err = codec.error()
+    enc_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in ev]))
+    f1 = (1 << 30) // 128
+    v1 = int(codec.bits[:f1].to(torch.int64).sum().item()) * 16
+    h = hashlib.sha256(struct.pack("<QQQ", 1 << 30, f1, v1))
+    h.update(codec.bits[:f1].cpu().numpy().tobytes())
+    h.update(codec.values[:v1].cpu().numpy().tobytes())
+    prefix_ok = seed == 42 and h.hexdigest() == GOLDEN_1GIB_U8_SHA
+    out = torch.empty_like(x)
+    d0, d1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    codec.decode(v, out=out)
+    d0.record(stream)
+    codec.decode(v, out=out)
+    d1.record(stream)
+    torch.cuda.synchronize()
+    dec_ms = d0.elapsed_time(d1)
+    ok = bool(torch.equal(out, x)) and err == 0 and codec.error() == 0
+    alg = n + codec.frames + v
+    res = {
+        "workload": f"FL encode of {n} u8 bytes (seed {seed}) on 1 GPU (BASELINE north star)",
+        "encode_ms": round(enc_ms, 4),
+        "encode_alg_GBps": round(alg / (enc_ms * 1e-3) / 1e9, 1),
+        "encode_input_GBps": round(n / (enc_ms * 1e-3) / 1e9, 1),
+        "frac": round(alg / (enc_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+        "target_frac": 0.70,
+        "decode_ms": round(dec_ms, 4),
+        "decode_alg_GBps": round(alg / (dec_ms * 1e-3) / 1e9, 1),
+        "roundtrip": ok,
+        "prefix_1GiB_matches_reference_fl_cpu": prefix_ok,
+    }
+    del x, out, codec
+    torch.cuda.empty_cache()
+    return res
 
 
 def rl_section(n: int, seed: int, steps: int, warmup: int, dev, cpu: bool):
@@ -279,6 +337,9 @@ def main():
         sample = min(n, 1 << 30) if args.cpu_sample < 0 else args.cpu_sample
         if world == 1 and sample > 0:
             cpu = cpu_baseline(args.kind, args.seed, sample, gpu_bits, gpu_values)
+        ns = None
+        if world == 1 and not args.no_north_star and not (n == 16 << 30 and args.kind == "u8"):
+            ns = north_star_section(args.seed, args.steps, args.warmup, dev)
         rl = None
         if world == 1 and not args.no_rl:
             rl = rl_section(n, args.seed, args.steps, args.warmup, dev, cpu=sample > 0)
@@ -325,6 +386,7 @@ def main():
             "cpu_baseline": cpu,
             "parity": parity,
             "rl": rl,
+            "north_star": ns,
         }
         print(json.dumps(line), flush=True)
     if world > 1:
