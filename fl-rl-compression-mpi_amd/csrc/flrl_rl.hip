@@ -23,11 +23,12 @@
 // its runs, staged per wave in LDS and stored contiguously.
 //
 // Decode: rl_offsets_kernel scans the counts (R bytes) into per-tile output
-// offsets (and validates them); rl_decode_kernel then expands each tile of
-// 4096 runs independently, in 32 KiB LDS output windows: the runs overlapping
-// a window memset their bytes into it with aligned dword stores, and the window
-// leaves in 16-byte stores (the two chunks a tile shares with its neighbours
-// byte by byte).
+// offsets (and validates them); rl_decode_kernel (3 workgroups per CU,
+// grid-stride, the next tile's counts and values prefetched into registers)
+// then expands each tile of 4096 runs independently, in 32 KiB LDS output
+// windows: the runs overlapping a window memset their bytes into it with
+// aligned dword stores, and the window leaves in 16-byte stores (the two chunks
+// a tile shares with its neighbours byte by byte).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdlib.h>
@@ -55,6 +56,7 @@ constexpr int kRlStageBytes = 16256;  // LDS run staging (2 workgroups of 64 KiB
 constexpr int kRdRuns = 4096;        // runs per decode tile
 constexpr int kRdThreads = 256;
 constexpr int kRdWindow = 32768;     // LDS output window (bytes)
+constexpr int kRdPerCU = 3;          // resident decode workgroups per CU (LDS 53 KB each)
 constexpr int kRoRunsPerThread = 256;
 constexpr int kRoRuns = kRoRunsPerThread * kThreads;  // runs per offsets workgroup
 static_assert(kRdRuns % kRoRunsPerThread == 0, "whole offsets lanes per decode tile");
@@ -728,7 +730,7 @@ __device__ __forceinline__ uint32_t run_lower(const uint32_t *pre, uint32_t nr, 
 
 __global__ __launch_bounds__(kRdThreads) void rl_decode_kernel(
     const uint8_t *__restrict__ counts, const uint8_t *__restrict__ values, uint64_t runs,
-    uint8_t *__restrict__ out, uint64_t n, const uint64_t *__restrict__ tile_base)
+    uint8_t *__restrict__ out, uint64_t n, const uint64_t *__restrict__ tile_base, uint64_t ntiles)
 {
     __shared__ uint32_t s_pre[kRdRuns + 1];  // local output offset of each run
     __shared__ u32x4 s_val4[kRdRuns / 16];
@@ -741,29 +743,38 @@ __global__ __launch_bounds__(kRdThreads) void rl_decode_kernel(
     const int tid = threadIdx.x;
     const int lane = tid & (kWave - 1);
     const int wave = tid / kWave;
-    const uint64_t tile = blockIdx.x;
-    const uint64_t r0 = tile * kRdRuns;
-    const uint64_t base = tile_base[tile];
-    const uint64_t end = tile_base[tile + 1];
-    if (end > n || base >= end)
-        return;  // empty, or malformed (flagged by rl_offsets_kernel)
-    const uint32_t nr = (uint32_t)(runs - r0 < (uint64_t)kRdRuns ? runs - r0 : kRdRuns);
-
-    // ---- counts -> block scan -> s_pre; values -> LDS ------------------------
     constexpr int RPT = kRdRuns / kRdThreads;
-    static_assert(RPT % 16 == 0, "whole 16-byte count vectors per thread");
+    static_assert(RPT == 16, "one 16-byte count vector and one value vector per thread");
+    // grid-stride over decode tiles; the next tile's counts, values and bounds
+    // are loaded into registers while this one is expanded
+    uint64_t tile = blockIdx.x;
+    if (tile >= ntiles)
+        return;
+    u32x4 cv = load16_tail(counts, tile * kRdRuns + tid * RPT, runs);
+    u32x4 vv = load16_tail(values, tile * kRdRuns + tid * RPT, runs);
+    uint64_t base = tile_base[tile], end = tile_base[tile + 1];
+    for (;;) {
+    const uint64_t r0 = tile * kRdRuns;
+    const uint64_t next = tile + gridDim.x;
+    __syncthreads();  // the previous tile's LDS readers are done
+    const bool skip = end > n || base >= end;  // empty, or malformed (flagged by rl_offsets_kernel)
+    const uint32_t nr = (uint32_t)(runs - r0 < (uint64_t)kRdRuns ? runs - r0 : kRdRuns);
     uint32_t c[RPT];
     uint32_t sum = 0;
+    s_val4[tid] = vv;
 #pragma unroll
-    for (int q = 0; q < RPT / 16; ++q) {
-        const u32x4 v = load16_tail(counts, r0 + tid * RPT + 16 * q, runs);
-        s_val4[(tid * RPT) / 16 + q] = load16_tail(values, r0 + tid * RPT + 16 * q, runs);
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            c[16 * q + i] = (v[i >> 2] >> (8 * (i & 3))) & 0xFFu;
-            sum += c[16 * q + i];
-        }
+    for (int i = 0; i < 16; ++i) {
+        c[i] = (cv[i >> 2] >> (8 * (i & 3))) & 0xFFu;
+        sum += c[i];
     }
+    const uint64_t cbase = base, cend = end;
+    if (next < ntiles) {
+        cv = load16_tail(counts, next * kRdRuns + tid * RPT, runs);
+        vv = load16_tail(values, next * kRdRuns + tid * RPT, runs);
+        base = tile_base[next];
+        end = tile_base[next + 1];
+    }
+    if (!skip) {
     const uint32_t inc = wave_incl_scan_u32(sum);
     if (lane == kWave - 1)
         s_wave[wave] = inc;
@@ -779,18 +790,18 @@ __global__ __launch_bounds__(kRdThreads) void rl_decode_kernel(
         run += c[i];
     }
     if (tid == 0)
-        s_pre[kRdRuns] = (uint32_t)(end - base);
+        s_pre[kRdRuns] = (uint32_t)(cend - cbase);
     __syncthreads();
 
     // ---- windows: the first run of a window is found by one binary search per
     // tile, later ones are handed on by the thread whose run crosses the
     // window end; a thread stops at the first run starting past the window
-    const uint64_t g0 = base & ~15ull;
+    const uint64_t g0 = cbase & ~15ull;
     uint32_t ja = run_lower(s_pre, nr, 0);
-    for (uint64_t gw = g0; gw < end; gw += kRdWindow) {
-        const uint32_t lo = (uint32_t)((gw > base ? gw : base) - base);  // owned, tile-local
-        const uint32_t hi = (uint32_t)((gw + kRdWindow < end ? gw + kRdWindow : end) - base);
-        const uint32_t shift = (uint32_t)(gw < base ? base - gw : 0);    // window pos of local lo
+    for (uint64_t gw = g0; gw < cend; gw += kRdWindow) {
+        const uint32_t lo = (uint32_t)((gw > cbase ? gw : cbase) - cbase);  // owned, tile-local
+        const uint32_t hi = (uint32_t)((gw + kRdWindow < cend ? gw + kRdWindow : cend) - cbase);
+        const uint32_t shift = (uint32_t)(gw < cbase ? cbase - gw : 0);    // window pos of local lo
         for (uint32_t j = ja + tid; j < nr && s_pre[j] < hi; j += kRdThreads) {
             uint32_t x = s_pre[j], y = s_pre[j + 1];  // s_pre[nr] = the tile's total
             if (y > hi)
@@ -814,18 +825,23 @@ __global__ __launch_bounds__(kRdThreads) void rl_decode_kernel(
         }
         __syncthreads();
         ja = s_next;
-        const uint32_t wlen = (uint32_t)(end - gw < (uint64_t)kRdWindow ? end - gw : kRdWindow);
+        const uint32_t wlen = (uint32_t)(cend - gw < (uint64_t)kRdWindow ? cend - gw : kRdWindow);
         for (uint32_t ch = tid; ch * 16 < wlen; ch += kRdThreads) {
             const uint64_t gp = gw + 16ull * ch;
-            if (gp >= base && gp + 16 <= end) {
+            if (gp >= cbase && gp + 16 <= cend) {
                 __builtin_nontemporal_store(s_win4[ch], reinterpret_cast<u32x4 *>(out + gp));
             } else {
                 for (uint32_t f = 0; f < 16; ++f)
-                    if (gp + f >= base && gp + f < end)
+                    if (gp + f >= cbase && gp + f < cend)
                         out[gp + f] = s_win[16 * ch + f];
             }
         }
         __syncthreads();
+    }
+    }
+    if (next >= ntiles)
+        break;
+    tile = next;
     }
 }
 
@@ -925,8 +941,9 @@ extern "C" int flrl_rl_decode_device(const uint8_t *d_counts, const uint8_t *d_v
                        (uint64_t)runs, (uint64_t)n, tile_base, (uint32_t)L.tiles,
                        (uint32_t)L.blocks, ctrl, status);
     FLRL_HIP(hipGetLastError());
-    hipLaunchKernelGGL(rl_decode_kernel, dim3((uint32_t)L.tiles), dim3(kRdThreads), 0, s, d_counts,
-                       d_values, (uint64_t)runs, d_out, (uint64_t)n, tile_base);
+    const size_t rgrid = (size_t)kRdPerCU * (size_t)cu_count();
+    hipLaunchKernelGGL(rl_decode_kernel, dim3((uint32_t)(L.tiles < rgrid ? L.tiles : rgrid)), dim3(kRdThreads), 0,
+                       s, d_counts, d_values, (uint64_t)runs, d_out, (uint64_t)n, tile_base, (uint64_t)L.tiles);
     FLRL_HIP(hipGetLastError());
     return FLRL_OK;
 }
