@@ -63,3 +63,14 @@ def test_file_format_helpers():
     assert r.input_size == 4 and r.counts.tolist() == [1, 3] and r.values.tolist() == [9, 8]
     with pytest.raises(ValueError):
         flrl.parse_fl_file(blob[:-1])
+
+
+def test_file_codec_needs_device(tmp_path):
+    if flrl.device_count() > 0:
+        pytest.skip("a HIP device is visible")
+    src = tmp_path / "in"
+    src.write_bytes(b"abc")
+    for fn in (flrl.fl_compress_file, flrl.fl_decompress_file):
+        with pytest.raises(flrl.FLRLError) as e:
+            fn(str(src), str(tmp_path / "out"), 1, 0)
+        assert e.value.code == flrl.E_NODEV

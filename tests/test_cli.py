@@ -105,3 +105,14 @@ def test_malformed_rl_files_rejected(cli_path, tmp_path):
     (tmp_path / "bad.rl").write_bytes(blob)
     r = run(cli_path, "d", "rl-cpu", tmp_path / "bad.rl", tmp_path / "o", check=False)
     assert r.returncode == 2
+
+
+@pytest.mark.parametrize("method", ["fl", "fl-nccl", "rl"])
+def test_gpu_methods_fail_loudly_without_device(cli_path, tmp_path, method):
+    if flrl.device_count() > 0:
+        pytest.skip("a HIP device is visible")
+    src, out = tmp_path / "in", tmp_path / "out"
+    src.write_bytes(bytes(range(200)))
+    r = subprocess.run([cli_path, "c", method, str(src), str(out)], capture_output=True, text=True)
+    assert r.returncode == 2 and "[ERROR]" in r.stderr
+    assert not out.exists()
