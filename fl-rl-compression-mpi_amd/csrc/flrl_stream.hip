@@ -98,6 +98,8 @@ bool pwrite_all(int fd, const void *src, size_t bytes, uint64_t off)
     return true;
 }
 
+size_t requested_or(size_t requested) { return requested ? requested : kDefaultChunk; }
+
 size_t chunk_size(size_t requested)
 {
     size_t c = requested ? requested : kDefaultChunk;
@@ -474,6 +476,406 @@ extern "C" int flrl_fl_decompress_file(const char *in_path, const char *out_path
             if (pend != SIZE_MAX && !finish(pend, pend_k))
                 break;
             pend = c;
+            pend_k = k;
+        }
+        if (!fail.failed.load() && pend != SIZE_MAX)
+            (void)finish(pend, pend_k);
+    };
+    std::vector<std::thread> threads;
+    for (int w = 0; w < nw; ++w)
+        threads.emplace_back(worker, w);
+    for (auto &t : threads)
+        t.join();
+    if (fail.failed.load())
+        return set_error(fail.code ? fail.code : FLRL_E_HIP, "%s", fail.msg.c_str());
+    if (::close(out.fd) != 0) {
+        out.fd = -1;
+        return set_error(FLRL_E_ARG, "[FileIO] Cannot write to file");
+    }
+    out.fd = -1;
+    return FLRL_OK;
+}
+
+// ---------------------------------------------------------------------------
+// RL, file to file. Chunks are encoded independently on the GPUs; the writer
+// stitches them in order: a run crossing a chunk boundary is re-split into
+// 255-byte pieces from its true start (IMPLEMENTATION-PLAN.md:125-147), so the
+// file equals a whole-input encode. A chunk's records split into its first run
+// (which may continue the pending run of earlier chunks), the runs wholly
+// inside it (written verbatim) and its last run (kept pending). Runs are
+// maximal, so consecutive records with one value are pieces of one run.
+// counts[] are written in place; values[] go to a side file appended at the
+// end, since R (and so the values offset) is known only then.
+// ---------------------------------------------------------------------------
+namespace flrl {
+namespace {
+
+struct RlWriter {
+    int out = -1, side = -1;
+    uint64_t runs = 0;                     // records written so far
+    uint8_t pend_v = 0;
+    uint64_t pend_len = 0;                 // pending run (0: none)
+    uint8_t fill_c[4096], fill_v[4096];
+    bool put(const uint8_t *c, const uint8_t *v, size_t k)
+    {
+        if (!k)
+            return true;
+        if (!pwrite_all(out, c, k, 16 + runs) || !pwrite_all(side, v, k, runs))
+            return false;
+        runs += k;
+        return true;
+    }
+    bool emit(uint8_t v, uint64_t len)  // one run of len bytes, split from its start
+    {
+        memset(fill_c, 255, sizeof(fill_c));
+        memset(fill_v, v, sizeof(fill_v));
+        uint64_t full = len / 255;
+        while (full) {
+            const size_t k = full < sizeof(fill_c) ? (size_t)full : sizeof(fill_c);
+            if (!put(fill_c, fill_v, k))
+                return false;
+            full -= k;
+        }
+        if (len % 255) {
+            const uint8_t c = (uint8_t)(len % 255);
+            return put(&c, &v, 1);
+        }
+        return true;
+    }
+    bool chunk(const uint8_t *cnt, const uint8_t *val, size_t R)
+    {
+        if (!R)
+            return true;
+        size_t j1 = 1;  // records of the chunk's first run
+        uint64_t l0 = cnt[0];
+        while (j1 < R && val[j1] == val[0])
+            l0 += cnt[j1++];
+        if (j1 == R) {  // the whole chunk is one run
+            if (pend_len && pend_v == val[0]) {
+                pend_len += l0;
+            } else {
+                if (pend_len && !emit(pend_v, pend_len))
+                    return false;
+                pend_v = val[0];
+                pend_len = l0;
+            }
+            return true;
+        }
+        size_t start = 0;
+        if (pend_len && pend_v == val[0]) {
+            if (!emit(pend_v, pend_len + l0))
+                return false;
+            start = j1;
+        } else if (pend_len && !emit(pend_v, pend_len)) {
+            return false;
+        }
+        size_t jl = R - 1;  // first record of the chunk's last run
+        uint64_t ll = cnt[R - 1];
+        while (jl > j1 && val[jl - 1] == val[R - 1])
+            ll += cnt[--jl];
+        if (!put(cnt + start, val + start, jl - start))
+            return false;
+        pend_v = val[R - 1];
+        pend_len = ll;
+        return true;
+    }
+};
+
+}  // namespace
+}  // namespace flrl
+
+extern "C" int flrl_rl_compress_file(const char *in_path, const char *out_path, int workers,
+                                     size_t chunk_bytes)
+{
+    clear_error();
+    if (!in_path || !out_path)
+        return set_error(FLRL_E_ARG, "flrl_rl_compress_file: null path");
+    int ndev = 0;
+    const int W = worker_count(workers, &ndev);
+    if (W <= 0)
+        return set_error(FLRL_E_NODEV, "flrl_rl_compress_file: no HIP device");
+    Fd in, out, side;
+    if ((in.fd = ::open(in_path, O_RDONLY)) < 0)
+        return set_error(FLRL_E_ARG, "[FileIO] Cannot open file: %s", in_path);
+    struct stat st;
+    if (::fstat(in.fd, &st) != 0)
+        return set_error(FLRL_E_ARG, "[FileIO] Cannot stat file: %s", in_path);
+    const uint64_t n = (uint64_t)st.st_size;
+    if ((out.fd = ::open(out_path, O_RDWR | O_CREAT | O_TRUNC, 0644)) < 0)
+        return set_error(FLRL_E_ARG, "[FileIO] Cannot open file: %s", out_path);
+    const std::string side_path = std::string(out_path) + ".values.tmp";
+    if ((side.fd = ::open(side_path.c_str(), O_RDWR | O_CREAT | O_TRUNC, 0600)) < 0)
+        return set_error(FLRL_E_ARG, "[FileIO] Cannot open file: %s", side_path.c_str());
+    ::unlink(side_path.c_str());  // anonymous from here on
+    const size_t chunk = requested_or(chunk_bytes);
+    const size_t nchunks = n ? (size_t)((n + chunk - 1) / chunk) : 0;
+
+    Failure fail;
+    std::mutex m;
+    std::condition_variable cv;
+    std::vector<Ready> ready(nchunks);
+    const int nw = (int)(W < (int)(nchunks ? nchunks : 1) ? W : (nchunks ? nchunks : 1));
+    std::vector<std::atomic<bool>> slot_free((size_t)nw * 2);
+    for (auto &f : slot_free)
+        f.store(true);
+
+    auto worker = [&](int w) {
+        if (hipSetDevice(w % ndev) != hipSuccess) {
+            fail.set(FLRL_E_HIP, "hipSetDevice failed");
+            cv.notify_all();
+            return;
+        }
+        Slots S;
+        if (S.alloc(chunk, chunk, chunk, flrl_rl_scratch_bytes(chunk)) != hipSuccess) {
+            fail.set(FLRL_E_NOMEM, "Cannot allocate memory");
+            cv.notify_all();
+            return;
+        }
+        auto finish = [&](size_t c, int k) -> bool {
+            Slot &x = S.slot[k];
+            if (hipStreamSynchronize(x.s) != hipSuccess)
+                return false;
+            const int kerr = flrl_scratch_error(x.d_scr, x.s);
+            if (kerr) {
+                fail.set(kerr, "rl encode: device error");
+                return false;
+            }
+            const size_t R = (size_t)x.h_u64[0];
+            if (hipMemcpyAsync(x.h_b, x.d_b, R, hipMemcpyDeviceToHost, x.s) != hipSuccess ||
+                hipMemcpyAsync(x.h_c, x.d_c, R, hipMemcpyDeviceToHost, x.s) != hipSuccess ||
+                hipStreamSynchronize(x.s) != hipSuccess)
+                return false;
+            std::atomic<bool> *rel = &slot_free[(size_t)w * 2 + k];
+            rel->store(false);
+            {
+                std::lock_guard<std::mutex> g(m);
+                Ready &r = ready[c];
+                r.bits = x.h_b;  // counts
+                r.values = x.h_c;
+                r.nbits = r.nvalues = R;
+                r.released = rel;
+                r.done = true;
+            }
+            cv.notify_all();
+            return true;
+        };
+        size_t pend = SIZE_MAX;
+        int pend_k = 0;
+        int i = 0;
+        for (size_t c = (size_t)w; c < nchunks && !fail.failed.load(); c += (size_t)nw, ++i) {
+            const int k = i & 1;
+            Slot &x = S.slot[k];
+            {
+                std::unique_lock<std::mutex> g(m);
+                cv.wait(g, [&] { return slot_free[(size_t)w * 2 + k].load() || fail.failed.load(); });
+            }
+            if (fail.failed.load())
+                break;
+            const uint64_t off = (uint64_t)c * chunk;
+            const size_t len = (size_t)((c + 1 == nchunks) ? n - off : chunk);
+            if (!pread_all(in.fd, x.h_a, len, off)) {
+                fail.set(FLRL_E_ARG, "[FileIO] Cannot read file content");
+                break;
+            }
+            if (hipMemcpyAsync(x.d_a, x.h_a, len, hipMemcpyHostToDevice, x.s) != hipSuccess ||
+                flrl_rl_encode_device(x.d_a, len, x.d_b, x.d_c, x.d_u64, x.d_scr, x.scr_bytes, x.s) != FLRL_OK ||
+                hipMemcpyAsync(x.h_u64, x.d_u64, 8, hipMemcpyDeviceToHost, x.s) != hipSuccess) {
+                fail.set(FLRL_E_HIP, std::string("rl encode: ") + flrl_last_error());
+                break;
+            }
+            if (pend != SIZE_MAX && !finish(pend, pend_k)) {
+                fail.set(FLRL_E_HIP, "rl encode: stream failed");
+                break;
+            }
+            pend = c;
+            pend_k = k;
+        }
+        if (!fail.failed.load() && pend != SIZE_MAX && !finish(pend, pend_k))
+            fail.set(FLRL_E_HIP, "rl encode: stream failed");
+        std::unique_lock<std::mutex> g(m);
+        cv.wait(g, [&] {
+            return fail.failed.load() ||
+                   (slot_free[(size_t)w * 2].load() && slot_free[(size_t)w * 2 + 1].load());
+        });
+    };
+    std::vector<std::thread> threads;
+    for (int w = 0; w < nw && nchunks; ++w)
+        threads.emplace_back(worker, w);
+
+    RlWriter wr;
+    wr.out = out.fd;
+    wr.side = side.fd;
+    for (size_t c = 0; c < nchunks; ++c) {
+        Ready r;
+        {
+            std::unique_lock<std::mutex> g(m);
+            cv.wait(g, [&] { return ready[c].done || fail.failed.load(); });
+            if (fail.failed.load())
+                break;
+            r.bits = ready[c].bits;
+            r.values = ready[c].values;
+            r.nbits = ready[c].nbits;
+            r.released = ready[c].released;
+        }
+        const bool ok = wr.chunk(r.bits, r.values, r.nbits);
+        {
+            std::lock_guard<std::mutex> g(m);
+            r.released->store(true);
+        }
+        cv.notify_all();
+        if (!ok) {
+            fail.set(FLRL_E_ARG, "[FileIO] Cannot write to file");
+            cv.notify_all();
+            break;
+        }
+    }
+    for (auto &t : threads)
+        t.join();
+    if (fail.failed.load())
+        return set_error(fail.code ? fail.code : FLRL_E_HIP, "%s", fail.msg.c_str());
+    if (wr.pend_len && !wr.emit(wr.pend_v, wr.pend_len))
+        return set_error(FLRL_E_ARG, "[FileIO] Cannot write to file");
+    // header, then values[] after counts[]
+    const uint64_t R = wr.runs;
+    const uint64_t hdr[2] = {n, R};
+    if (!pwrite_all(out.fd, hdr, sizeof(hdr), 0))
+        return set_error(FLRL_E_ARG, "[FileIO] Cannot write to file");
+    {
+        std::vector<uint8_t> buf(R < (4u << 20) ? (size_t)R + 1 : (4u << 20));
+        for (uint64_t o = 0; o < R;) {
+            const size_t k = (size_t)(R - o < buf.size() ? R - o : buf.size());
+            if (!pread_all(side.fd, buf.data(), k, o) || !pwrite_all(out.fd, buf.data(), k, 16 + R + o))
+                return set_error(FLRL_E_ARG, "[FileIO] Cannot write to file");
+            o += k;
+        }
+    }
+    if (::ftruncate(out.fd, (off_t)(16 + 2 * R)) != 0)
+        return set_error(FLRL_E_ARG, "[FileIO] Cannot write to file");
+    if (::close(out.fd) != 0) {
+        out.fd = -1;
+        return set_error(FLRL_E_ARG, "[FileIO] Cannot write to file");
+    }
+    out.fd = -1;
+    return FLRL_OK;
+}
+
+extern "C" int flrl_rl_decompress_file(const char *in_path, const char *out_path, int workers,
+                                       size_t chunk_bytes)
+{
+    clear_error();
+    if (!in_path || !out_path)
+        return set_error(FLRL_E_ARG, "flrl_rl_decompress_file: null path");
+    int ndev = 0;
+    const int W = worker_count(workers, &ndev);
+    if (W <= 0)
+        return set_error(FLRL_E_NODEV, "flrl_rl_decompress_file: no HIP device");
+    Fd in, out;
+    if ((in.fd = ::open(in_path, O_RDONLY)) < 0)
+        return set_error(FLRL_E_ARG, "[FileIO] Cannot open file: %s", in_path);
+    struct stat st;
+    if (::fstat(in.fd, &st) != 0)
+        return set_error(FLRL_E_ARG, "[FileIO] Cannot stat file: %s", in_path);
+    const uint64_t fsize = (uint64_t)st.st_size;
+    uint64_t hdr[2];
+    if (fsize < 16 || !pread_all(in.fd, hdr, sizeof(hdr), 0))
+        return set_error(FLRL_E_FORMAT, "[FileIO] truncated RL header");
+    const uint64_t n = hdr[0], R = hdr[1];
+    if (R > fsize || 16 + 2 * R != fsize)
+        return set_error(FLRL_E_FORMAT, "[FileIO] RL runs %llu do not match the file (%llu bytes)",
+                         (unsigned long long)R, (unsigned long long)fsize);
+    const size_t chunk = requested_or(chunk_bytes) < 256 ? 256 : requested_or(chunk_bytes);
+    // blocks of runs with at most `chunk` output bytes (a run is <= 255 bytes)
+    struct Block {
+        uint64_t r0, r1, o0;
+    };
+    std::vector<Block> blocks;
+    {
+        std::vector<uint8_t> buf(1u << 22);
+        uint64_t out_pos = 0, r0 = 0, acc = 0;
+        for (uint64_t o = 0; o < R;) {
+            const size_t k = (size_t)(R - o < buf.size() ? R - o : buf.size());
+            if (!pread_all(in.fd, buf.data(), k, 16 + o))
+                return set_error(FLRL_E_ARG, "[FileIO] Cannot read file content");
+            for (size_t i = 0; i < k; ++i) {
+                const uint32_t c = buf[i];
+                if (c == 0)
+                    return set_error(FLRL_E_FORMAT, "RL count 0 at run %llu", (unsigned long long)(o + i));
+                if (acc && acc + c > chunk) {
+                    blocks.push_back({r0, o + i, out_pos});
+                    out_pos += acc;
+                    r0 = o + i;
+                    acc = 0;
+                }
+                acc += c;
+            }
+            o += k;
+        }
+        if (R) {
+            blocks.push_back({r0, R, out_pos});
+            out_pos += acc;
+        }
+        if (out_pos != n)
+            return set_error(FLRL_E_FORMAT, "RL counts sum to %llu, header says %llu",
+                             (unsigned long long)out_pos, (unsigned long long)n);
+    }
+    if ((out.fd = ::open(out_path, O_WRONLY | O_CREAT | O_TRUNC, 0644)) < 0)
+        return set_error(FLRL_E_ARG, "[FileIO] Cannot open file: %s", out_path);
+    if (::ftruncate(out.fd, (off_t)n) != 0)
+        return set_error(FLRL_E_ARG, "[FileIO] Cannot write to file");
+    const size_t nb = blocks.size();
+    Failure fail;
+    const int nw = nb ? (int)(W < (int)nb ? W : (int)nb) : 0;
+    auto worker = [&](int w) {
+        if (hipSetDevice(w % ndev) != hipSuccess) {
+            fail.set(FLRL_E_HIP, "hipSetDevice failed");
+            return;
+        }
+        Slots S;
+        if (S.alloc(chunk, chunk, chunk, flrl_rl_decode_scratch_bytes(chunk)) != hipSuccess) {
+            fail.set(FLRL_E_NOMEM, "Cannot allocate memory");
+            return;
+        }
+        auto len_of = [&](size_t b) {
+            return (size_t)((b + 1 < nb ? blocks[b + 1].o0 : n) - blocks[b].o0);
+        };
+        auto finish = [&](size_t b, int k) -> bool {
+            Slot &x = S.slot[k];
+            if (hipStreamSynchronize(x.s) != hipSuccess)
+                return false;
+            const int kerr = flrl_scratch_error(x.d_scr, x.s);
+            if (kerr) {
+                fail.set(kerr, "rl decode: malformed counts");
+                return false;
+            }
+            if (!pwrite_all(out.fd, x.h_c, len_of(b), blocks[b].o0)) {
+                fail.set(FLRL_E_ARG, "[FileIO] Cannot write to file");
+                return false;
+            }
+            return true;
+        };
+        size_t pend = SIZE_MAX;
+        int pend_k = 0;
+        int i = 0;
+        for (size_t b = (size_t)w; b < nb && !fail.failed.load(); b += (size_t)nw, ++i) {
+            const int k = i & 1;  // slot k last held block b - 2*nw, written in the previous iteration
+            Slot &x = S.slot[k];
+            const size_t nr = (size_t)(blocks[b].r1 - blocks[b].r0);
+            const size_t len = len_of(b);
+            if (!pread_all(in.fd, x.h_a, nr, 16 + blocks[b].r0) ||
+                !pread_all(in.fd, x.h_b, nr, 16 + R + blocks[b].r0)) {
+                fail.set(FLRL_E_ARG, "[FileIO] Cannot read file content");
+                break;
+            }
+            if (hipMemcpyAsync(x.d_a, x.h_a, nr, hipMemcpyHostToDevice, x.s) != hipSuccess ||
+                hipMemcpyAsync(x.d_b, x.h_b, nr, hipMemcpyHostToDevice, x.s) != hipSuccess ||
+                flrl_rl_decode_device(x.d_a, x.d_b, nr, x.d_c, len, x.d_scr, x.scr_bytes, x.s) != FLRL_OK ||
+                hipMemcpyAsync(x.h_c, x.d_c, len, hipMemcpyDeviceToHost, x.s) != hipSuccess) {
+                fail.set(FLRL_E_HIP, std::string("rl decode: ") + flrl_last_error());
+                break;
+            }
+            if (pend != SIZE_MAX && !finish(pend, pend_k))
+                break;
+            pend = b;
             pend_k = k;
         }
         if (!fail.failed.load() && pend != SIZE_MAX)

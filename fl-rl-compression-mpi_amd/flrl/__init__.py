@@ -99,6 +99,8 @@ _sig("flrl_fl_decompress", ctypes.c_int, _sz, _vp, _sz, _vp, _sz,
      ctypes.POINTER(_u8p), ctypes.POINTER(_sz))
 _sig("flrl_fl_compress_file", ctypes.c_int, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int, _sz)
 _sig("flrl_fl_decompress_file", ctypes.c_int, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int, _sz)
+_sig("flrl_rl_compress_file", ctypes.c_int, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int, _sz)
+_sig("flrl_rl_decompress_file", ctypes.c_int, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int, _sz)
 _sig("flrl_fl_scratch_bytes", _sz, _sz)
 _sig("flrl_fl_values_capacity", _sz, _sz)
 _sig("flrl_fl_encode_device", ctypes.c_int, _vp, _sz, _vp, _vp, _vp, _vp, _sz, _vp)
@@ -203,6 +205,18 @@ def fl_compress_file(in_path: str, out_path: str, workers: int = 1, chunk_bytes:
 def fl_decompress_file(in_path: str, out_path: str, workers: int = 1, chunk_bytes: int = 0) -> None:
     """.fl file -> file streamed through the GPU(s); validates header and widths."""
     _check(_lib.flrl_fl_decompress_file(os.fsencode(in_path), os.fsencode(out_path), workers,
+                                        chunk_bytes))
+
+
+def rl_compress_file(in_path: str, out_path: str, workers: int = 1, chunk_bytes: int = 0) -> None:
+    """File -> .rl file streamed through the GPU(s) (runs re-split across chunks)."""
+    _check(_lib.flrl_rl_compress_file(os.fsencode(in_path), os.fsencode(out_path), workers,
+                                      chunk_bytes))
+
+
+def rl_decompress_file(in_path: str, out_path: str, workers: int = 1, chunk_bytes: int = 0) -> None:
+    """.rl file -> file streamed through the GPU(s); validates header and counts."""
+    _check(_lib.flrl_rl_decompress_file(os.fsencode(in_path), os.fsencode(out_path), workers,
                                         chunk_bytes))
 
 

@@ -4,11 +4,10 @@
 //   compress d <method> <input> <output>     decompress a file
 //
 // fl / fl-mpi / fl-nccl / fl-shmem / rl run on the GPU through the C ABI in
-// include/flrl.h (libflrl.so); fl-cpu / rl-cpu run the host codec. The FL GPU
-// methods stream the file through the GPUs in frame-aligned chunks
-// (flrl_fl_compress_file / flrl_fl_decompress_file: `fl` one pipeline, the
-// multi-GPU methods one per GPU), so neither the file nor its output is held in
-// memory; FLRL_CHUNK_BYTES and FLRL_WORKERS override the chunk size (64 MiB)
+// include/flrl.h (libflrl.so); fl-cpu / rl-cpu run the host codec. The GPU
+// methods stream the file through the GPUs in chunks (flrl_{fl,rl}_*_file:
+// `fl` and `rl` one pipeline, the multi-GPU FL methods one per GPU), so
+// neither the file nor its output is held in memory; FLRL_CHUNK_BYTES and FLRL_WORKERS override the chunk size (64 MiB)
 // and the pipeline count. Errors print
 // "[ERROR]: <message>" to stderr like the reference (main.cu:95-98), but the
 // process then exits with status 2 instead of 0, and no partial output file is
@@ -64,15 +63,20 @@ size_t env_size(const char *name, size_t dflt)
     return (v && *v) ? (size_t)std::strtoull(v, nullptr, 0) : dflt;
 }
 
-// FL on the GPU(s), file to file: one call does load + encode/decode + save.
+// FL / RL on the GPU(s), file to file: one call does load + encode/decode + save.
 bool fl_streamed(const Args &a, bool compress_op)
 {
-    if (a.method != Method::FixedLength && a.method != Method::FixedLengthMulti)
+    const bool rl = a.method == Method::RunLength;
+    if (a.method != Method::FixedLength && a.method != Method::FixedLengthMulti && !rl)
         return false;
-    const int workers = (int)env_size("FLRL_WORKERS", a.method == Method::FixedLength ? 1 : 0);
+    const int workers = (int)env_size("FLRL_WORKERS", a.method == Method::FixedLengthMulti ? 0 : 1);
     const size_t chunk = env_size("FLRL_CHUNK_BYTES", 0);
     Timer t;
-    if (compress_op)
+    if (rl && compress_op)
+        check(flrl_rl_compress_file(a.inputFile, a.outputFile, workers, chunk), "rl compress");
+    else if (rl)
+        check(flrl_rl_decompress_file(a.inputFile, a.outputFile, workers, chunk), "rl decompress");
+    else if (compress_op)
         check(flrl_fl_compress_file(a.inputFile, a.outputFile, workers, chunk), "fl compress");
     else
         check(flrl_fl_decompress_file(a.inputFile, a.outputFile, workers, chunk), "fl decompress");

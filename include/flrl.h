@@ -104,6 +104,16 @@ int flrl_fl_compress_sharded(const uint8_t *data, size_t size, int ngpus, flrl_f
 int flrl_fl_compress_file(const char *in_path, const char *out_path, int workers, size_t chunk_bytes);
 int flrl_fl_decompress_file(const char *in_path, const char *out_path, int workers, size_t chunk_bytes);
 
+/* RL, file to file, same pipelines (the CLI's `c|d rl`). Compression encodes
+ * chunks independently and re-splits a run that crosses a chunk boundary from
+ * its true start, so the file equals flrl_rl_compress + the RL container;
+ * values[] go through an unlinked side file until R is known. Decompression
+ * validates the header (file length == 16 + 2*runs), every count (>= 1) and
+ * their sum (== inputSize), then decodes blocks of runs of <= chunk_bytes
+ * output (0: 64 MiB; at least 256) on all pipelines. */
+int flrl_rl_compress_file(const char *in_path, const char *out_path, int workers, size_t chunk_bytes);
+int flrl_rl_decompress_file(const char *in_path, const char *out_path, int workers, size_t chunk_bytes);
+
 /* ---- FL, device-resident (asynchronous on `stream`) -----------------------
  * Replaces FixedLength::gpuCompressDevice (src/fl/fl_gpu.cuh:17,
  * fl_gpu.cu:425-535) — outputs stay in HBM.

@@ -152,3 +152,94 @@ def test_large_file_default_chunks(tmp_path):
     del blob
     flrl.fl_decompress_file(str(dst), str(back), 2, 0)
     assert back.read_bytes() == data.tobytes()
+
+
+# ---- RL file path -------------------------------------------------------------
+
+def _oracle_rl_file(data: np.ndarray) -> bytes:
+    counts, values = oracle.rl_compress(data)
+    return flrl.rl_file_bytes(data.size, counts, values)
+
+
+def _rl_input(kind: str, n: int, seed: int = 9) -> np.ndarray:
+    if kind == "spans":  # runs far longer than a chunk, some exact multiples of 255
+        a = np.zeros(n, np.uint8)
+        a[n // 3:] = 7
+        a[n // 3 + 255 * 40: n // 3 + 255 * 80] = 9
+        a[-1] = 1
+        return a
+    return oracle.gen(kind, n, seed)
+
+
+@pytest.mark.parametrize("kind,n", [("runs32", 1), ("runs32", 255), ("runs32", 256), ("runs32", 100_003),
+                                    ("longruns", 300_007), ("zero", 70_000), ("u8", 65_537),
+                                    ("spans", 200_000)])
+@pytest.mark.parametrize("chunk,workers", [(1000, 3), (4096, 1), (65536, 2), (0, 1)])
+def test_rl_compress_file_matches_oracle(tmp_path, kind, n, chunk, workers):
+    data = _rl_input(kind, n)
+    src, dst, back = tmp_path / "in", tmp_path / "out.rl", tmp_path / "back"
+    data.tofile(src)
+    flrl.rl_compress_file(str(src), str(dst), workers, chunk)
+    assert dst.read_bytes() == _oracle_rl_file(data)
+    flrl.rl_decompress_file(str(dst), str(back), workers, chunk)
+    assert back.read_bytes() == data.tobytes()
+
+
+def test_rl_file_empty_and_one_chunk_per_byte(tmp_path):
+    src, dst, back = tmp_path / "in", tmp_path / "out.rl", tmp_path / "back"
+    src.write_bytes(b"")
+    flrl.rl_compress_file(str(src), str(dst), 2, 0)
+    assert dst.read_bytes() == bytes(16)
+    flrl.rl_decompress_file(str(dst), str(back), 2, 0)
+    assert back.read_bytes() == b""
+    data = _rl_input("spans", 3000)
+    data.tofile(src)
+    flrl.rl_compress_file(str(src), str(dst), 3, 1)  # every byte its own chunk
+    assert dst.read_bytes() == _oracle_rl_file(data)
+
+
+def test_rl_file_large_default_chunks(tmp_path):
+    n = (200 << 20) + 12345
+    data = oracle.gen("runs32", n, 42)
+    src, dst, back = tmp_path / "in", tmp_path / "out.rl", tmp_path / "back"
+    data.tofile(src)
+    flrl.rl_compress_file(str(src), str(dst), 2, 0)
+    assert hashlib.sha256(dst.read_bytes()).digest() == hashlib.sha256(_oracle_rl_file(data)).digest()
+    flrl.rl_decompress_file(str(dst), str(back), 3, 0)
+    assert back.read_bytes() == data.tobytes()
+
+
+def test_rl_malformed_files_rejected(tmp_path):
+    data = _rl_input("runs32", 5000)
+    good = _oracle_rl_file(data)
+    n, R = struct.unpack_from("<QQ", good)
+
+    def bad(blob, name):
+        p = tmp_path / name
+        p.write_bytes(blob)
+        with pytest.raises(flrl.FLRLError) as e:
+            flrl.rl_decompress_file(str(p), str(tmp_path / (name + ".out")), 2, 1024)
+        return e.value.code
+
+    assert bad(good[:10], "short") == 4
+    assert bad(good[:-1], "trunc") == 4
+    assert bad(struct.pack("<QQ", n + 1, R) + good[16:], "sum") == 4
+    b = bytearray(good)
+    b[16 + 5] = 0
+    assert bad(bytes(b), "zero") == 4
+
+
+def test_cli_rl_streamed(cli_path, tmp_path):
+    data = _rl_input("longruns", 400_001, 3)
+    src = tmp_path / "in"
+    data.tofile(src)
+    ref = tmp_path / "ref.rl"
+    subprocess.run([cli_path, "c", "rl-cpu", str(src), str(ref)], check=True, capture_output=True)
+    env = dict(os.environ, FLRL_CHUNK_BYTES="777", FLRL_WORKERS="3")
+    out, back = tmp_path / "o.rl", tmp_path / "back"
+    r = subprocess.run([cli_path, "c", "rl", str(src), str(out)], env=env, capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    assert out.read_bytes() == ref.read_bytes()
+    r = subprocess.run([cli_path, "d", "rl", str(out), str(back)], env=env, capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    assert back.read_bytes() == data.tobytes()
