@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """End-to-end FL file rates (file I/O + PCIe included), for DESIGN.md.
 
-Compares, on one synthetic input file:
+Compares, on one synthetic input file (u8 for FL, runs32 for RL):
   whole   read file -> flrl_fl_compress (host buffers: H2D, encode, D2H,
           synchronous, the reference gpuCompress shape) -> write .fl
   stream  flrl_fl_compress_file (chunked, pipelined; workers = 1 and = GPUs)
@@ -67,6 +67,30 @@ def main():
         assert open(dst, "rb").read() == ref, "streamed file differs"
         res[f"stream_w{w}_decompress_GBps"] = n / best(lambda: flrl.fl_decompress_file(dst, back, w, 0), a.reps) / 1e9
     res["files_identical"] = True
+    # RL on runs32 of the same size
+    data = flrl.gen_host("runs32", n, 42)
+    data.tofile(src)
+    del data
+
+    def rl_whole_c():
+        x = open(src, "rb").read()
+        c = flrl.rl_compress(x)
+        with open(dst, "wb") as f:
+            f.write(c.to_file_bytes())
+
+    def rl_whole_d():
+        c = flrl.parse_rl_file(open(dst, "rb").read())
+        flrl.rl_decompress(c.input_size, c.counts, c.values).tofile(back)
+
+    rl_whole_c()
+    res["rl_whole_compress_GBps"] = n / best(rl_whole_c, a.reps) / 1e9
+    res["rl_whole_decompress_GBps"] = n / best(rl_whole_d, a.reps) / 1e9
+    ref = open(dst, "rb").read()
+    for w in sorted({1, 2, max(1, flrl.device_count())}):
+        res[f"rl_stream_w{w}_compress_GBps"] = n / best(lambda: flrl.rl_compress_file(src, dst, w, 0), a.reps) / 1e9
+        assert open(dst, "rb").read() == ref, "streamed RL file differs"
+        res[f"rl_stream_w{w}_decompress_GBps"] = n / best(lambda: flrl.rl_decompress_file(dst, back, w, 0), a.reps) / 1e9
+    res["rl_files_identical"] = True
     for p in (src, dst, back):
         os.remove(p)
     os.rmdir(d)
