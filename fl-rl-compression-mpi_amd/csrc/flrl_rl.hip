@@ -762,6 +762,7 @@ __global__ __launch_bounds__(kRdThreads) void rl_decode_kernel(
     uint32_t c[RPT];
     uint32_t sum = 0;
     s_val4[tid] = vv;
+    const u32x4 vv_cur = vv;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
         c[i] = (cv[i >> 2] >> (8 * (i & 3))) & 0xFFu;
@@ -783,7 +784,8 @@ __global__ __launch_bounds__(kRdThreads) void rl_decode_kernel(
 #pragma unroll
     for (int v = 0; v < kRdThreads / kWave; ++v)
         before += v < wave ? s_wave[v] : 0u;
-    uint32_t run = before + inc - sum;
+    const uint32_t run0 = before + inc - sum;  // output offset of this thread's first run
+    uint32_t run = run0;
 #pragma unroll
     for (int i = 0; i < RPT; ++i) {
         s_pre[tid * RPT + i] = run;
@@ -791,12 +793,37 @@ __global__ __launch_bounds__(kRdThreads) void rl_decode_kernel(
     }
     if (tid == 0)
         s_pre[kRdRuns] = (uint32_t)(cend - cbase);
+    const uint64_t g0 = cbase & ~15ull;
+    if (cend - g0 <= (uint64_t)kRdWindow) {
+        // the whole tile fits one window (short runs): every thread memsets its
+        // own 16 runs from registers, no LDS look-ups
+        const uint32_t shift = (uint32_t)(cbase - g0);
+        uint32_t p = run0 + shift;
+#pragma unroll
+        for (int i = 0; i < RPT; ++i) {
+            const uint8_t v = (uint8_t)(vv_cur[i >> 2] >> (8 * (i & 3)));
+            const uint32_t q = p + c[i];
+            for (; p < q; ++p)
+                s_win[p] = v;
+        }
+        __syncthreads();
+        const uint32_t wlen = (uint32_t)(cend - g0);
+        for (uint32_t ch = tid; ch * 16 < wlen; ch += kRdThreads) {
+            const uint64_t gp = g0 + 16ull * ch;
+            if (gp >= cbase && gp + 16 <= cend) {
+                __builtin_nontemporal_store(s_win4[ch], reinterpret_cast<u32x4 *>(out + gp));
+            } else {
+                for (uint32_t f = 0; f < 16; ++f)
+                    if (gp + f >= cbase && gp + f < cend)
+                        out[gp + f] = s_win[16 * ch + f];
+            }
+        }
+    } else {
     __syncthreads();
 
     // ---- windows: the first run of a window is found by one binary search per
     // tile, later ones are handed on by the thread whose run crosses the
     // window end; a thread stops at the first run starting past the window
-    const uint64_t g0 = cbase & ~15ull;
     uint32_t ja = run_lower(s_pre, nr, 0);
     for (uint64_t gw = g0; gw < cend; gw += kRdWindow) {
         const uint32_t lo = (uint32_t)((gw > cbase ? gw : cbase) - cbase);  // owned, tile-local
@@ -837,6 +864,7 @@ __global__ __launch_bounds__(kRdThreads) void rl_decode_kernel(
             }
         }
         __syncthreads();
+    }
     }
     }
     if (next >= ntiles)
