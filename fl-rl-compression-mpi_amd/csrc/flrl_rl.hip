@@ -11,16 +11,17 @@
 // iff it is natural or c == 0, and then c becomes 1, else c = (c+1) mod 255.
 // Each head h emits the run that ENDS at h-1 (count = c before h, value =
 // x[h-1]); the tile holding byte n-1 emits the final run, so no tile needs
-// bytes of its successor. A 64 KiB tile sits in LDS (LDS-DMA) and each lane
-// owns 128 contiguous bytes of it, so a lane holds at most one split head
-// (before its first natural head). Within the tile two 32-bit scans suffice: a
-// PhaseMap scan of lane states (constant after a natural head, else
-// "+L mod 255") and a sum of the heads that do not depend on the tile's
-// incoming state (those from its first natural head on). Across tiles ONE
-// decoupled look-back composes segment maps {bytes before the first natural
-// head, heads from it on, state after} into (heads before the tile, state at
-// its start); every lane then knows its global head index and state and emits
-// its runs, staged per wave in LDS and stored contiguously.
+// bytes of its successor. A tile is two 64 KiB sub-tiles that pass through LDS
+// one after the other (LDS-DMA); each lane owns 128 contiguous bytes of a
+// sub-tile, so a lane holds at most one split head (before its first natural
+// head). Within a sub-tile two 32-bit scans suffice: a PhaseMap scan of lane
+// states (constant after a natural head, else "+L mod 255") and a sum of the
+// heads that do not depend on the tile's incoming state (those from its first
+// natural head on), whose runs are staged in LDS as the sub-tiles go by.
+// Across tiles ONE decoupled look-back per tile composes segment maps {bytes
+// before the first natural head, heads from it on, state after} into (heads
+// before the tile, state at its start); then only the split heads before the
+// first natural head are written and the staged runs leave contiguously.
 //
 // Decode: rl_offsets_kernel scans the counts (R bytes) into per-tile output
 // offsets (and validates them); rl_decode_kernel (3 workgroups per CU,
@@ -49,7 +50,8 @@ namespace flrl {
 
 constexpr int kRlThreads = 512;                     // encode workgroup: 8 waves
 constexpr int kRlLaneBytes = 128;                   // contiguous bytes per lane
-constexpr int kRlTileBytes = kRlLaneBytes * kRlThreads;  // 64 KiB, held in LDS
+constexpr int kRlSub = 2;                           // sub-tiles per tile (one look-back each tile)
+constexpr int kRlTileBytes = kRlLaneBytes * kRlThreads * kRlSub;  // 2 x 64 KiB sub-tiles through LDS
 constexpr int kRlLookG = 1;      // look-back granules per lane (window 64 G tiles)
 constexpr int kRlStageBytes = 16256;  // LDS run staging (2 workgroups of 64 KiB tiles per CU)
 
@@ -285,18 +287,23 @@ __device__ __forceinline__ uint64_t lookback_seg(uint64_t *status, uint32_t tile
     }
 }
 
-// One tile of T/64 waves x 64 lanes x LB bytes per workgroup, in ticket order.
-// The tile lands in LDS by LDS-DMA (global_load_lds, 1 KiB per wave-instruction,
-// coalesced), swizzled so that every lane then reads ITS OWN contiguous LB bytes
-// conflict-free: lane row r keeps chunk c at r*LB + ((c ^ (r & 7)) * 16).
+// One tile of SUB sub-tiles per workgroup, in ticket order; a sub-tile is
+// T/64 waves x 64 lanes x LB bytes and sits in LDS (LDS-DMA, 1 KiB per
+// wave-instruction, coalesced), swizzled so that every lane then reads ITS OWN
+// contiguous LB bytes conflict-free: row r keeps chunk c at r*LB + ((c^(r&7))*16).
 // Per lane: natural-head masks, count, first/last natural head. LB < 255, so a
-// lane holds at most one split head, and only before its first natural head;
-// lane phase maps and the counts of state-independent heads (those from the
-// tile's first natural head on) then need two cheap 32-bit wave scans. The
-// tile's composite map goes through the look-back; every lane then knows its
-// global head index and chunk state and emits its runs in order: staged per
-// wave in LDS and stored contiguously, or (dense waves) one lane row at a time.
-template <int T, int LB>
+// lane holds at most one split head, and only before its first natural head.
+// Two 32-bit wave scans per sub-tile: PhaseMaps (lane states relative to the
+// tile's incoming state) and the count of heads that do not depend on that
+// state (all heads from the tile's first natural head on), whose runs are
+// staged in LDS at their tile-local index while the sub-tiles stream through.
+// The tile's composite map then goes through ONE look-back (one per SUB
+// sub-tiles); the c_in-dependent prefix (split heads before the first natural
+// head, and the count of the run that head ends) is written after it and the
+// staged records leave contiguously. A tile with more state-independent runs
+// than the staging area holds (dense data) re-reads its sub-tiles after the
+// look-back and emits per wave.
+template <int T, int LB, int SUB>
 __global__ __launch_bounds__(T) void rl_encode_kernel(
     const uint8_t *__restrict__ in, uint64_t n, uint32_t ntiles, uint8_t *__restrict__ counts,
     uint8_t *__restrict__ values, uint64_t *__restrict__ runs_out, Ctrl *ctrl, uint64_t *status)
@@ -304,17 +311,17 @@ __global__ __launch_bounds__(T) void rl_encode_kernel(
     constexpr int W = T / kWave;
     constexpr int CH = LB / 16;  // 16-byte chunks per lane
     constexpr int WB = kWave * LB;
-    constexpr int TB = WB * W;
-    constexpr int SW = kRlStageBytes / W / 2;  // staged records per wave
+    constexpr int TB = WB * W;   // sub-tile bytes
+    constexpr int SW = kRlStageBytes / W / 2;  // per-wave staged records (dense path)
+    constexpr int SC = kRlStageBytes / 2;      // tile staging: runs
     static_assert(LB == 128, "the swizzle and the 2 x u64 head masks assume 8 chunks per lane");
-    // ONE LDS object: [tile image][per-wave staging: counts | values][small]
+    // ONE LDS object: [sub-tile image][staging: counts | values][small]
     __shared__ __attribute__((aligned(16))) uint8_t s_lds[TB + kRlStageBytes + 128];
     uint8_t *const img = s_lds;
+    uint8_t *const tsc = s_lds + TB;
+    uint8_t *const tsv = tsc + SC;
     uint8_t *const stc = s_lds + TB + (size_t)(threadIdx.x / kWave) * 2 * SW;
     uint8_t *const stv = stc + SW;
-    constexpr int SC = kRlStageBytes / 2;  // tile staging: runs
-    uint8_t *const tsc = s_lds + TB;        // counts[SC] | values[SC] (same bytes as the per-wave areas)
-    uint8_t *const tsv = tsc + SC;
     uint32_t *const s_wmap = reinterpret_cast<uint32_t *>(s_lds + TB + kRlStageBytes);
     uint32_t *const s_wfirst = s_wmap + W;
     uint32_t *const s_wh = s_wfirst + W;
@@ -325,139 +332,109 @@ __global__ __launch_bounds__(T) void rl_encode_kernel(
     const int tid = threadIdx.x;
     const int lane = tid & (kWave - 1);
     const int w = tid / kWave;
+    const uint32_t row = (uint32_t)tid;  // lane row within a sub-tile
+    const uint32_t o = row * LB;          // its byte offset in the sub-tile
+    const uint8_t *my = img + o;
     FLRL_RL_PHASE_BEGIN();
     const uint32_t tile = take_ticket(ctrl, s_ticket);
-    const uint64_t tile_off = (uint64_t)tile * TB;
-    const uint64_t wave_off = tile_off + (uint64_t)w * WB;
+    const uint64_t tile_off = (uint64_t)tile * (SUB * TB);
+    const uint32_t tile_len = (uint32_t)(n - tile_off < (uint64_t)(SUB * TB) ? n - tile_off : SUB * TB);
 
-    // ---- tile -> LDS. Instruction j of wave w fills rows w*64 + j*8 .. +7;
-    // lane writes row j*8 + lane/8 at column lane&7, i.e. chunk (lane&7)^(row&7)
-    {
-        const uint32_t c = ((uint32_t)lane & 7u) ^ (((uint32_t)lane >> 3) & 7u);
-        uint8_t *dst = img + w * WB;
-        if (wave_off + WB <= n) {
+    // ---- one sub-tile into LDS, natural heads, lane/wave/tile phase scans ---
+    struct Sub {
+        uint32_t nat[CH / 2];  // 16-bit masks, two per word
+        uint32_t ncnt, fpos, lpos, vbl, p0;
+        uint32_t lrel;   // lane start state from the sub-tile's start (PhaseMap)
+        uint32_t smap;   // the sub-tile's PhaseMap
+        uint32_t sfirst; // first natural head in the sub-tile (0xFFFFFFFF: none)
+        uint64_t off;    // sub-tile offset in the input
+    };
+    auto scan_sub = [&](int s, Sub &L) {
+        L.off = tile_off + (uint64_t)s * TB;
+        const uint64_t wave_off = L.off + (uint64_t)w * WB;
+        {
+            const uint32_t c = ((uint32_t)lane & 7u) ^ (((uint32_t)lane >> 3) & 7u);
+            uint8_t *dst = img + w * WB;
+            if (wave_off + WB <= n) {
 #pragma unroll
-            for (int j = 0; j < WB / 1024; ++j) {
-                const uint8_t *src = in + wave_off + (uint32_t)(j * 8 + lane / 8) * LB + c * 16;
-                __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)src,
-                                                 (__attribute__((address_space(3))) void *)(dst + j * 1024),
-                                                 16, 0, 0);
-            }
-        } else {
+                for (int j = 0; j < WB / 1024; ++j) {
+                    const uint8_t *src = in + wave_off + (uint32_t)(j * 8 + lane / 8) * LB + c * 16;
+                    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)src,
+                                                     (__attribute__((address_space(3))) void *)(dst + j * 1024),
+                                                     16, 0, 0);
+                }
+            } else {
 #pragma unroll
-            for (int j = 0; j < WB / 1024; ++j) {
-                const uint64_t g = wave_off + (uint32_t)(j * 8 + lane / 8) * LB + c * 16;
-                *reinterpret_cast<u32x4 *>(dst + j * 1024 + lane * 16) = load16_tail(in, g, n);
+                for (int j = 0; j < WB / 1024; ++j) {
+                    const uint64_t g = wave_off + (uint32_t)(j * 8 + lane / 8) * LB + c * 16;
+                    *reinterpret_cast<u32x4 *>(dst + j * 1024 + lane * 16) = load16_tail(in, g, n);
+                }
             }
         }
-    }
-    const uint32_t row = (uint32_t)tid;  // lane row within the tile
-    const uint32_t o = row * LB;          // its byte offset in the tile
-    const uint64_t lane_off = tile_off + o;
-    const uint32_t vbl = lane_off >= n ? 0u : (n - lane_off >= LB ? (uint32_t)LB : (uint32_t)(n - lane_off));
-    const uint32_t ptile = (tid == 0 && tile_off > 0) ? in[tile_off - 1] : 0u;
-    __syncthreads();  // waits for the LDS-DMA too
-    FLRL_RL_PHASE(0);
-
-    const uint8_t *my = img + o;
-    auto chunk = [&](int c) -> u32x4 {
-        return *reinterpret_cast<const u32x4 *>(my + ((c ^ (row & 7u)) * 16));
-    };
-    const uint32_t p0 = row == 0 ? ptile : img[(row - 1) * LB + ((7u ^ ((row - 1) & 7u)) * 16) + 15];
-
-    // ---- pass 1: natural heads ----------------------------------------------
-    uint32_t nat[CH / 2];  // 16-bit masks, two per word
-    uint32_t ncnt = 0, fpos = LB, lpos = 0;
-    {
-        uint32_t p = p0;
+        const uint64_t lane_off = L.off + o;
+        L.vbl = lane_off >= n ? 0u : (n - lane_off >= LB ? (uint32_t)LB : (uint32_t)(n - lane_off));
+        const uint32_t pstart = (tid == 0 && L.off > 0) ? in[L.off - 1] : 0u;
+        __syncthreads();  // waits for the LDS-DMA too
+        L.p0 = row == 0 ? pstart : img[(row - 1) * LB + ((7u ^ ((row - 1) & 7u)) * 16) + 15];
+        L.ncnt = 0;
+        L.fpos = LB;
+        L.lpos = 0;
+        uint32_t p = L.p0;
 #pragma unroll
         for (int c = 0; c < CH; ++c) {
-            const u32x4 x = chunk(c);
-            const uint32_t vb = vbl > 16u * c ? (vbl - 16u * c >= 16 ? 16u : vbl - 16u * c) : 0u;
+            const u32x4 x = *reinterpret_cast<const u32x4 *>(my + ((c ^ (row & 7u)) * 16));
+            const uint32_t vb = L.vbl > 16u * c ? (L.vbl - 16u * c >= 16 ? 16u : L.vbl - 16u * c) : 0u;
             uint32_t m = nat_mask(x, p) & (vb >= 16 ? 0xFFFFu : ((1u << vb) - 1u));
             if (c == 0 && lane_off == 0)
                 m |= 1u;
             if (c & 1)
-                nat[c / 2] |= m << 16;
+                L.nat[c / 2] |= m << 16;
             else
-                nat[c / 2] = m;
+                L.nat[c / 2] = m;
             p = x.w >> 24;
-            ncnt += __popc(m);
+            L.ncnt += __popc(m);
             if (m) {
-                fpos = fpos == (uint32_t)LB ? 16u * c + (__ffs(m) - 1) : fpos;
-                lpos = 16u * c + (31u - __clz(m));
+                L.fpos = L.fpos == (uint32_t)LB ? 16u * c + (__ffs(m) - 1) : L.fpos;
+                L.lpos = 16u * c + (31u - __clz(m));
             }
         }
-    }
-    const bool has = ncnt != 0;
-    // lane phase map, wave scan (exclusive), first natural head of the wave
-    const uint32_t lmap = has ? pm_make(true, vbl - lpos) : pm_make(false, vbl);
-    const uint32_t incl = wave_incl_scan_map(lmap);
-    uint32_t lexcl = __shfl_up(incl, 1, kWave);
-    lexcl = lane == 0 ? kMapIdent : lexcl;
-    {
-        const unsigned long long hb = __ballot(has);
-        const int fl = hb ? __ffsll(hb) - 1 : 0;
-        const uint32_t ff = (uint32_t)__shfl(fpos, fl, kWave);
-        if (lane == kWave - 1)
-            s_wmap[w] = incl;
-        if (lane == 0)
-            s_wfirst[w] = hb ? (uint32_t)(w * WB + fl * LB) + ff : 0xFFFFFFFFu;
-    }
-    __syncthreads();
-    uint32_t tile_map = kMapIdent, wave_pre = kMapIdent, tile_first = 0xFFFFFFFFu;
-#pragma unroll
-    for (int v = 0; v < W; ++v) {
-        if (v == w)
-            wave_pre = tile_map;
-        tile_map = pm_compose(tile_map, s_wmap[v]);
-        if (tile_first == 0xFFFFFFFFu && s_wfirst[v] != 0xFFFFFFFFu)
-            tile_first = s_wfirst[v];
-    }
-    const uint32_t tile_len = (uint32_t)(n - tile_off < (uint64_t)TB ? n - tile_off : TB);
-    const uint32_t lane_rel = pm_compose(wave_pre, lexcl);  // lane start state from the tile's
-
-    // ---- heads that do not depend on the tile's incoming state: all heads from
-    // the tile's first natural head on. After it, lane start states are
-    // constants of the scan; the lane holding it counts its natural heads only.
-    uint32_t indep = 0;
-    if (tile_first != 0xFFFFFFFFu && o + LB > tile_first) {
-        indep = ncnt;
-        if (o > tile_first) {
-            const uint32_t cr = pm_apply(lane_rel, 1);  // any stand-in incoming state
-            const uint32_t j0 = cr == 0 ? 0u : 255u - cr;
-            indep += (j0 < fpos && j0 < vbl) ? 1u : 0u;
+        const bool has = L.ncnt != 0;
+        const uint32_t lmap = has ? pm_make(true, L.vbl - L.lpos) : pm_make(false, L.vbl);
+        const uint32_t incl = wave_incl_scan_map(lmap);
+        uint32_t lexcl = __shfl_up(incl, 1, kWave);
+        lexcl = lane == 0 ? kMapIdent : lexcl;
+        {
+            const unsigned long long hb = __ballot(has);
+            const int fl = hb ? __ffsll(hb) - 1 : 0;
+            const uint32_t ff = (uint32_t)__shfl(L.fpos, fl, kWave);
+            if (lane == kWave - 1)
+                s_wmap[w] = incl;
+            if (lane == 0)
+                s_wfirst[w] = hb ? (uint32_t)(w * WB + fl * LB) + ff : 0xFFFFFFFFu;
         }
-    }
-    const uint32_t hincl = wave_incl_scan_u32(indep);
-    if (lane == kWave - 1)
-        s_wh[w] = hincl;
-    __syncthreads();
-    uint32_t K = 0, wave_hbase = 0;
+        __syncthreads();
+        uint32_t smap = kMapIdent, wave_pre = kMapIdent, sfirst = 0xFFFFFFFFu;
 #pragma unroll
-    for (int v = 0; v < W; ++v) {
-        wave_hbase += v < w ? s_wh[v] : 0u;
-        K += s_wh[v];
-    }
-    const uint32_t pre = K ? tile_first : tile_len;
-    const uint64_t tmap = K ? sm_nat(tile_first, K, tile_map & 0xFFu) : sm_nonat(tile_len);
-    FLRL_RL_PHASE(1);
-
-    // ---- stage the runs that do not depend on the incoming state (all heads
-    // from the tile's first natural head on) at their tile-local index, while
-    // wave 0 resolves the look-back: waves 1.. stage first, wave 0 after
-    const bool staged = K <= (uint32_t)SC;  // tile-uniform
-    auto stage_lane = [&]() {
-        if (!K || o + LB <= tile_first)
-            return;  // no state-independent head in this lane
-        const bool after = o > tile_first;  // else: the lane holding the first natural head
-        const uint32_t cr = after ? pm_apply(lane_rel, 1) : 0u;  // constant after it
-        const uint32_t j0 = cr == 0 ? 0u : 255u - cr;
-        const bool split = after && j0 < fpos && j0 < vbl;
-        uint64_t h0 = 0, h1 = 0;
+        for (int v = 0; v < W; ++v) {
+            if (v == w)
+                wave_pre = smap;
+            smap = pm_compose(smap, s_wmap[v]);
+            if (sfirst == 0xFFFFFFFFu && s_wfirst[v] != 0xFFFFFFFFu)
+                sfirst = s_wfirst[v];
+        }
+        L.smap = smap;
+        L.sfirst = sfirst;
+        L.lrel = pm_compose(wave_pre, lexcl);
+    };
+    // lane head masks, given the lane's start state c0 and whether a split
+    // before its first natural head counts
+    auto head_masks = [&](const Sub &L, uint32_t c0, bool with_split, uint64_t &h0, uint64_t &h1) {
+        const uint32_t j0 = c0 == 0 ? 0u : 255u - c0;
+        const bool split = with_split && j0 < L.fpos && j0 < L.vbl;
+        h0 = h1 = 0;
 #pragma unroll
         for (int c = 0; c < CH; ++c) {
-            uint32_t h = (nat[c / 2] >> (16 * (c & 1))) & 0xFFFFu;
+            uint32_t h = (L.nat[c / 2] >> (16 * (c & 1))) & 0xFFFFu;
             if (split && (j0 >> 4) == (uint32_t)c)
                 h |= 1u << (j0 & 15u);
             if (c < 4)
@@ -465,7 +442,11 @@ __global__ __launch_bounds__(T) void rl_encode_kernel(
             else
                 h1 |= (uint64_t)h << (16 * (c - 4));
         }
-        uint32_t slot = wave_hbase + (hincl - indep);
+    };
+    // a lane's runs in order from head masks: count = distance to the previous
+    // head (the lane's first: c_first + pos), value = the byte before the head
+    auto lane_runs = [&](const Sub &L, uint64_t h0, uint64_t h1, uint32_t c_first, uint8_t *sc, uint8_t *sv,
+                         uint32_t slot) {
         int prev = -1;
         while (h0 | h1) {
             int pos;
@@ -476,19 +457,69 @@ __global__ __launch_bounds__(T) void rl_encode_kernel(
                 pos = 64 + __builtin_ctzll(h1);
                 h1 &= h1 - 1;
             }
-            // the tile's first record (the first natural head) gets its count later
-            uint32_t cnt = prev < 0 ? add_c(cr, (uint32_t)pos) : (uint32_t)(pos - prev);
+            uint32_t cnt = prev < 0 ? add_c(c_first, (uint32_t)pos) : (uint32_t)(pos - prev);
             cnt = cnt == 0 ? 255u : cnt;
             const uint32_t q = (uint32_t)pos - 1;
-            const uint32_t val = pos == 0 ? p0 : my[(((q >> 4) ^ (row & 7u)) * 16) + (q & 15u)];
-            tsc[slot] = (uint8_t)cnt;
-            tsv[slot] = (uint8_t)val;
+            const uint32_t val = pos == 0 ? L.p0 : my[(((q >> 4) ^ (row & 7u)) * 16) + (q & 15u)];
+            sc[slot] = (uint8_t)cnt;
+            sv[slot] = (uint8_t)val;
             ++slot;
             prev = pos;
         }
     };
-    if (staged && w != 0)
-        stage_lane();
+
+    // ---- sub-tiles: stage the state-independent runs ------------------------
+    uint32_t rel_in = kMapIdent;       // PhaseMap from the tile start to this sub-tile
+    uint32_t first = 0xFFFFFFFFu;      // the tile's first natural head (tile-relative)
+    uint32_t K = 0;                    // state-independent heads staged so far
+    bool staged = true;
+    uint8_t v0 = 0;                    // the tile's first byte
+    for (int s = 0; s < SUB; ++s) {
+        if (tile_off + (uint64_t)s * TB >= n)
+            break;  // tile-uniform
+        if (s > 0)
+            __syncthreads();  // the previous sub-tile's LDS readers are done
+        Sub L;
+        scan_sub(s, L);
+        if (s == 0)
+            v0 = img[0];
+        const bool seen = first != 0xFFFFFFFFu;  // a natural head before this sub-tile
+        const uint32_t lrel = pm_compose(rel_in, L.lrel);
+        uint32_t indep = 0;
+        bool lane_indep = false, after = false;
+        if (seen) {
+            lane_indep = after = true;
+        } else if (L.sfirst != 0xFFFFFFFFu && o + LB > L.sfirst) {
+            lane_indep = true;
+            after = o > L.sfirst;
+        }
+        const uint32_t cr = after ? pm_apply(lrel, 1) : 0u;  // constant after the first head
+        uint64_t h0 = 0, h1 = 0;
+        if (lane_indep) {
+            head_masks(L, cr, after, h0, h1);
+            indep = (uint32_t)(__popcll(h0) + __popcll(h1));
+        }
+        const uint32_t hincl = wave_incl_scan_u32(indep);
+        if (lane == kWave - 1)
+            s_wh[w] = hincl;
+        __syncthreads();
+        uint32_t ks = 0, wave_hbase = 0;
+#pragma unroll
+        for (int v = 0; v < W; ++v) {
+            wave_hbase += v < w ? s_wh[v] : 0u;
+            ks += s_wh[v];
+        }
+        staged = staged && K + ks <= (uint32_t)SC;  // tile-uniform
+        if (staged && indep)
+            lane_runs(L, h0, h1, cr, tsc, tsv, K + wave_hbase + (hincl - indep));
+        if (!seen && L.sfirst != 0xFFFFFFFFu)
+            first = (uint32_t)s * TB + L.sfirst;
+        K += ks;
+        rel_in = pm_compose(rel_in, L.smap);
+    }
+    const uint32_t pre = first != 0xFFFFFFFFu ? first : tile_len;
+    const uint64_t tmap = first != 0xFFFFFFFFu ? sm_nat(first, K, rel_in & 0xFFu) : sm_nonat(tile_len);
+    FLRL_RL_PHASE(1);
 
     // ---- one look-back: (heads before the tile, chunk state at its start) --
     if (w == 0) {
@@ -496,8 +527,6 @@ __global__ __launch_bounds__(T) void rl_encode_kernel(
         const uint64_t state = lookback_seg<kRlLookG>(status, tile, tmap, ctrl);
         if (lane == 0)
             *s_state = state;
-        if (staged)
-            stage_lane();
     }
     __syncthreads();
     FLRL_RL_PHASE(2);
@@ -506,7 +535,6 @@ __global__ __launch_bounds__(T) void rl_encode_kernel(
     const uint32_t S = splits(c_in, pre);  // split heads before the first natural head
     if (staged) {
         // split heads h_in + s end full 255-byte chunks of the tile's first byte
-        const uint8_t v0 = img[0];
         for (uint32_t j = (uint32_t)tid; j < S; j += T) {
             const uint64_t gi = h_in + j;
             if (gi > 0) {
@@ -517,7 +545,7 @@ __global__ __launch_bounds__(T) void rl_encode_kernel(
         const uint64_t g0 = h_in + S;  // global index of the first natural head
         if (K) {
             if (tid == 0 && g0 > 0) {
-                const uint32_t c = add_c(c_in, tile_first);
+                const uint32_t c = add_c(c_in, first);
                 counts[g0 - 1] = (uint8_t)(c == 0 ? 255u : c);
                 values[g0 - 1] = tsv[0];
             }
@@ -527,110 +555,93 @@ __global__ __launch_bounds__(T) void rl_encode_kernel(
             }
         }
     } else {
-    // dense tile (more than SC state-independent runs): emit after the look-back
-    const uint32_t c_lane = pm_apply(lane_rel, c_in);
-    uint64_t g = (K && o > tile_first) ? h_in + S + wave_hbase + (hincl - indep) : h_in + splits(c_in, o);
-
-    // ---- head masks with the true states, then the lane's runs in order -----
-    uint64_t hm0 = 0, hm1 = 0;  // chunks 0-3 / 4-7
-    {
-        const uint32_t j0 = c_lane == 0 ? 0u : 255u - c_lane;
-        const bool split = j0 < fpos && j0 < vbl;
+        // dense tile: re-read each sub-tile and emit with the true states
+        uint32_t rel = kMapIdent;
+        uint64_t hb = h_in;  // heads before the sub-tile
+        for (int s = 0; s < SUB; ++s) {
+            if (tile_off + (uint64_t)s * TB >= n)
+                break;
+            __syncthreads();
+            Sub L;
+            scan_sub(s, L);
+            const uint32_t c_lane = pm_apply(pm_compose(rel, L.lrel), c_in);
+            uint64_t hm0, hm1;
+            head_masks(L, c_lane, true, hm0, hm1);
+            const uint32_t hl = (uint32_t)(__popcll(hm0) + __popcll(hm1));
+            const uint32_t hincl = wave_incl_scan_u32(hl);
+            if (lane == kWave - 1)
+                s_wh[w] = hincl;
+            __syncthreads();
+            uint32_t hs = 0, wave_hbase = 0;
 #pragma unroll
-        for (int c = 0; c < CH; ++c) {
-            uint32_t h = (nat[c / 2] >> (16 * (c & 1))) & 0xFFFFu;
-            if (split && (j0 >> 4) == (uint32_t)c)
-                h |= 1u << (j0 & 15u);
-            if (c < 4)
-                hm0 |= (uint64_t)h << (16 * c);
-            else
-                hm1 |= (uint64_t)h << (16 * (c - 4));
-        }
-    }
-    const uint32_t lane_heads_n = (uint32_t)(__popcll(hm0) + __popcll(hm1));
-    const uint32_t wave_heads = (uint32_t)wave_sum_u64((uint64_t)lane_heads_n);
-    if (wave_heads <= (uint32_t)SW) {
-        // sparse: each lane stages its runs at (g - first g of the wave) in LDS,
-        // then the wave stores them contiguously
-        const uint64_t gw = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(g >> 32), 0) << 32) |
-                            (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)g, 0);
-        uint32_t slot = (uint32_t)(g - gw);
-        int prev = -1;  // position of the previous head in this lane
-        while (hm0 | hm1) {
-            int pos;
-            if (hm0) {
-                pos = __builtin_ctzll(hm0);
-                hm0 &= hm0 - 1;
-            } else {
-                pos = 64 + __builtin_ctzll(hm1);
-                hm1 &= hm1 - 1;
+            for (int v = 0; v < W; ++v) {
+                wave_hbase += v < w ? s_wh[v] : 0u;
+                hs += s_wh[v];
             }
-            uint32_t cnt = prev < 0 ? add_c(c_lane, (uint32_t)pos) : (uint32_t)(pos - prev);
-            cnt = cnt == 0 ? 255u : cnt;
-            uint32_t val;
-            if (pos == 0) {
-                val = p0;
-            } else {
-                const uint32_t q = (uint32_t)pos - 1;
-                val = my[(((q >> 4) ^ (row & 7u)) * 16) + (q & 15u)];
-            }
-            stc[slot] = (uint8_t)cnt;
-            stv[slot] = (uint8_t)val;
-            ++slot;
-            prev = pos;
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        for (uint32_t j = lane; j < wave_heads; j += kWave) {
-            const uint64_t gi = gw + j;
-            if (gi > 0) {
-                counts[gi - 1] = stc[j];
-                values[gi - 1] = stv[j];
-            }
-        }
-    } else {
-        // dense: the wave emits ONE lane row at a time, lane t taking byte
-        // positions t and 64 + t of the row (ranks by popcount), so every
-        // store instruction stays contiguous
-        const uint64_t below = ((uint64_t)1 << lane) - 1;
-#pragma unroll 1
-        for (int r = 0; r < kWave; ++r) {
-            const uint64_t h0 = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(hm0 >> 32), r) << 32) |
-                                (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)hm0, r);
-            const uint64_t h1 = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(hm1 >> 32), r) << 32) |
-                                (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)hm1, r);
-            const uint64_t g_row = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(g >> 32), r) << 32) |
-                                   (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)g, r);
-            const uint32_t c_row = (uint32_t)__builtin_amdgcn_readlane((int)c_lane, r);
-            const uint32_t p_row = (uint32_t)__builtin_amdgcn_readlane((int)p0, r);
-            const uint32_t rr = (uint32_t)(w * kWave + r);
-            const uint8_t *rowp = img + rr * LB;
-#pragma unroll
-            for (int half = 0; half < 2; ++half) {
-                const uint64_t hm = half ? h1 : h0;
-                if ((hm >> lane) & 1u) {
-                    const uint64_t bl = hm & below;
-                    const uint32_t pos = (uint32_t)(half * 64 + lane);
-                    const uint32_t rank = (half ? (uint32_t)__popcll(h0) : 0u) + (uint32_t)__popcll(bl);
-                    int prev;
-                    if (bl)
-                        prev = half * 64 + 63 - __builtin_clzll(bl);
-                    else
-                        prev = (half && h0) ? 63 - __builtin_clzll(h0) : -1;
-                    uint32_t cnt = prev < 0 ? add_c(c_row, pos) : pos - (uint32_t)prev;
-                    cnt = cnt == 0 ? 255u : cnt;
-                    const uint32_t q = pos - 1;
-                    const uint32_t val = pos == 0 ? p_row : rowp[(((q >> 4) ^ (rr & 7u)) * 16) + (q & 15u)];
-                    const uint64_t gi = g_row + rank;
+            uint64_t g = hb + wave_hbase + (hincl - hl);
+            const uint32_t wave_heads = (uint32_t)wave_sum_u64((uint64_t)hl);
+            if (wave_heads <= (uint32_t)SW) {
+                // sparse wave: stage at (g - first g of the wave), store contiguously
+                const uint64_t gw = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(g >> 32), 0) << 32) |
+                                    (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)g, 0);
+                lane_runs(L, hm0, hm1, c_lane, stc, stv, (uint32_t)(g - gw));
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                for (uint32_t j = lane; j < wave_heads; j += kWave) {
+                    const uint64_t gi = gw + j;
                     if (gi > 0) {
-                        counts[gi - 1] = (uint8_t)cnt;
-                        values[gi - 1] = (uint8_t)val;
+                        counts[gi - 1] = stc[j];
+                        values[gi - 1] = stv[j];
+                    }
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            } else {
+                // dense wave: ONE lane row at a time, lane t taking byte positions
+                // t and 64 + t of the row (ranks by popcount): contiguous stores
+                const uint64_t below = ((uint64_t)1 << lane) - 1;
+#pragma unroll 1
+                for (int r = 0; r < kWave; ++r) {
+                    const uint64_t h0 = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(hm0 >> 32), r) << 32) |
+                                        (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)hm0, r);
+                    const uint64_t h1 = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(hm1 >> 32), r) << 32) |
+                                        (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)hm1, r);
+                    const uint64_t g_row = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(g >> 32), r) << 32) |
+                                           (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)g, r);
+                    const uint32_t c_row = (uint32_t)__builtin_amdgcn_readlane((int)c_lane, r);
+                    const uint32_t p_row = (uint32_t)__builtin_amdgcn_readlane((int)L.p0, r);
+                    const uint32_t rr = (uint32_t)(w * kWave + r);
+                    const uint8_t *rowp = img + rr * LB;
+#pragma unroll
+                    for (int half = 0; half < 2; ++half) {
+                        const uint64_t hm = half ? h1 : h0;
+                        if ((hm >> lane) & 1u) {
+                            const uint64_t bl = hm & below;
+                            const uint32_t pos = (uint32_t)(half * 64 + lane);
+                            const uint32_t rank = (half ? (uint32_t)__popcll(h0) : 0u) + (uint32_t)__popcll(bl);
+                            int prev;
+                            if (bl)
+                                prev = half * 64 + 63 - __builtin_clzll(bl);
+                            else
+                                prev = (half && h0) ? 63 - __builtin_clzll(h0) : -1;
+                            uint32_t cnt = prev < 0 ? add_c(c_row, pos) : pos - (uint32_t)prev;
+                            cnt = cnt == 0 ? 255u : cnt;
+                            const uint32_t q = pos - 1;
+                            const uint32_t val = pos == 0 ? p_row : rowp[(((q >> 4) ^ (rr & 7u)) * 16) + (q & 15u)];
+                            const uint64_t gi = g_row + rank;
+                            if (gi > 0) {
+                                counts[gi - 1] = (uint8_t)cnt;
+                                values[gi - 1] = (uint8_t)val;
+                            }
+                        }
                     }
                 }
             }
+            hb += hs;
+            rel = pm_compose(rel, L.smap);
         }
-    }
     }
     FLRL_RL_PHASE(3);
     FLRL_RL_PHASE_END();
@@ -638,7 +649,7 @@ __global__ __launch_bounds__(T) void rl_encode_kernel(
     // ---- the final run (ends at byte n-1) ----------------------------------
     if (tile + 1 == ntiles && tid == 0) {
         const uint64_t R = h_in + S + K;
-        const uint32_t c_end = pm_apply(tile_map, c_in);
+        const uint32_t c_end = pm_apply(rel_in, c_in);
         counts[R - 1] = (uint8_t)(c_end == 0 ? 255u : c_end);
         values[R - 1] = in[n - 1];
         *runs_out = R;
@@ -926,7 +937,7 @@ extern "C" int flrl_rl_encode_device(const uint8_t *d_in, size_t n, uint8_t *d_c
         return set_error(FLRL_E_ARG, "flrl_rl_encode_device: input too large");
     Ctrl *ctrl = static_cast<Ctrl *>(d_scratch);
     uint64_t *status = reinterpret_cast<uint64_t *>(ctrl + 1);
-    hipLaunchKernelGGL((rl_encode_kernel<kRlThreads, kRlLaneBytes>), dim3((uint32_t)L.tiles), dim3(kRlThreads), 0, s,
+    hipLaunchKernelGGL((rl_encode_kernel<kRlThreads, kRlLaneBytes, kRlSub>), dim3((uint32_t)L.tiles), dim3(kRlThreads), 0, s,
                        d_in, (uint64_t)n, (uint32_t)L.tiles, d_counts, d_values, d_runs, ctrl, status);
     FLRL_HIP(hipGetLastError());
     return FLRL_OK;

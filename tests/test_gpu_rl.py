@@ -53,7 +53,7 @@ def test_empty():
 
 
 SIZES = [1, 2, 15, 16, 17, 255, 256, 257, 1023, 1024, 1025, 16383, 16384, 16385,
-         131071, 131072, 131073, 300_001, (1 << 20) + 7]
+         65535, 65536, 65537, 131071, 131072, 131073, 196609, 300_001, (1 << 20) + 7]
 
 
 @pytest.mark.parametrize("n", SIZES)
@@ -63,7 +63,7 @@ def test_sizes_vs_oracle(n, kind):
 
 
 @pytest.mark.parametrize("L", [254, 255, 256, 509, 510, 511, 16384 + 3, 131072 + 255, 400_000])
-@pytest.mark.parametrize("start", [0, 1, 15, 16, 1023, 16380, 131070])
+@pytest.mark.parametrize("start", [0, 1, 15, 16, 1023, 16380, 65535, 65536, 131070])
 def test_long_run_splits(L, start):
     # one long run of 7s starting at `start` inside random data
     rng = np.random.default_rng(L + start)
@@ -88,6 +88,27 @@ def test_runs_spanning_many_tiles():
         v = (v + 1 + int(rng.integers(0, 200))) % 256
         total += L
     check(np.concatenate(parts))
+
+
+@pytest.mark.parametrize("quiet", [1, 65536 - 3, 65536 + 100, 131072 + 5])
+def test_first_natural_head_late(quiet):
+    # no natural head for `quiet` bytes (in the first sub-tile, at the sub-tile
+    # boundary, in the second sub-tile, in the next tile), then mixed data
+    rng = np.random.default_rng(quiet)
+    a = rng.integers(0, 4, size=quiet + 300_000, dtype=np.uint8)
+    a[:quiet] = 5
+    a[quiet] = 6
+    check(a)
+
+
+@pytest.mark.parametrize("maxrun", [6, 12, 20, 40])
+def test_medium_density(maxrun):
+    # mean runs around the staging threshold (state-independent runs per tile
+    # vs the LDS staging capacity): both emission paths, mixed per tile
+    rng = np.random.default_rng(maxrun)
+    lens = rng.integers(1, maxrun + 1, size=400_000)
+    vals = (np.cumsum(rng.integers(1, 255, size=lens.size)) % 256).astype(np.uint8)
+    check(np.repeat(vals, lens)[:2_000_003])
 
 
 def test_all_zero_large():
