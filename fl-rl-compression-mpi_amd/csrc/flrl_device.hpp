@@ -83,15 +83,24 @@ __device__ __forceinline__ uint32_t or_8lanes(uint32_t o)
     return o;
 }
 
+// DPP move from a lower lane (row_shr:k within 16-lane rows; row_bcast:15 /
+// row_bcast:31 across rows); lanes without a source (and rows outside RM) read 0.
+template <int CTRL, int RM>
+__device__ __forceinline__ uint32_t dpp_up0(uint32_t v)
+{
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, RM, 0xF, true);
+}
+
+// Inclusive wave scan in six DPP steps (no LDS crossbar round trips):
+// row_shr 1/2/4/8 scan each row, row_bcast:15 and :31 carry row totals up.
 __device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t v)
 {
-    const int lane = threadIdx.x & (kWave - 1);
-#pragma unroll
-    for (int o = 1; o < kWave; o <<= 1) {
-        const uint32_t t = __shfl_up(v, o, kWave);
-        if (lane >= o)
-            v += t;
-    }
+    v += dpp_up0<0x111, 0xF>(v);
+    v += dpp_up0<0x112, 0xF>(v);
+    v += dpp_up0<0x114, 0xF>(v);
+    v += dpp_up0<0x118, 0xF>(v);
+    v += dpp_up0<0x142, 0xA>(v);
+    v += dpp_up0<0x143, 0xC>(v);
     return v;
 }
 

@@ -45,6 +45,14 @@
 #define FLRL_RL_PHASE(k) ((void)0)
 #define FLRL_RL_PHASE_END() ((void)0)
 #endif
+// Per-tile timestamp hooks for scripts/ubench_rl.hip -DTRACE (no-ops here).
+// Extra dynamic LDS per encode workgroup (occupancy experiments only).
+#ifndef FLRL_RL_DYN_LDS
+#define FLRL_RL_DYN_LDS 0
+#endif
+#ifndef FLRL_RL_TRACE
+#define FLRL_RL_TRACE(tile, k) ((void)0)
+#endif
 
 namespace flrl {
 
@@ -85,32 +93,33 @@ __device__ __forceinline__ uint32_t pm_apply(uint32_t m, uint32_t c)
     const uint32_t v = c + (m & 0xFFu);
     return v >= 255u ? v - 255u : v;
 }
+// inclusive PhaseMap scan, DPP steps as wave_incl_scan_u32 (0 = identity map)
 __device__ __forceinline__ uint32_t wave_incl_scan_map(uint32_t m)
 {
-    const int lane = threadIdx.x & (kWave - 1);
-#pragma unroll
-    for (int o = 1; o < kWave; o <<= 1) {
-        const uint32_t t = __shfl_up(m, o, kWave);
-        if (lane >= o)
-            m = pm_compose(t, m);
-    }
+    m = pm_compose(dpp_up0<0x111, 0xF>(m), m);
+    m = pm_compose(dpp_up0<0x112, 0xF>(m), m);
+    m = pm_compose(dpp_up0<0x114, 0xF>(m), m);
+    m = pm_compose(dpp_up0<0x118, 0xF>(m), m);
+    m = pm_compose(dpp_up0<0x142, 0xA>(m), m);
+    m = pm_compose(dpp_up0<0x143, 0xC>(m), m);
     return m;
 }
 
-// 16-bit mask of bytes of x that differ from their predecessor (p = byte before).
+// 16-bit mask of bytes of x that differ from their predecessor (p = byte before):
+// SWAR non-zero test of x ^ (x shifted by a byte) leaves 0x80 in each differing
+// byte, and byte dot products with 2^k weights gather those top bits in order.
 __device__ __forceinline__ uint32_t nat_mask(u32x4 x, uint32_t p)
 {
     const uint32_t y0 = (x.x << 8) | (p & 0xFFu), y1 = (x.y << 8) | (x.x >> 24);
     const uint32_t y2 = (x.z << 8) | (x.y >> 24), y3 = (x.w << 8) | (x.z >> 24);
     const uint32_t d[4] = {x.x ^ y0, x.y ^ y1, x.z ^ y2, x.w ^ y3};
-    uint32_t m = 0;
+    uint32_t nz[4];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const uint32_t nz = (((d[q] & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | d[q]) & 0x80808080u;
-        const uint32_t b4 = ((nz >> 7) & 1u) | ((nz >> 14) & 2u) | ((nz >> 21) & 4u) | ((nz >> 28) & 8u);
-        m |= b4 << (4 * q);
-    }
-    return m;
+    for (int q = 0; q < 4; ++q)
+        nz[q] = (((d[q] & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | d[q]) & 0x80808080u;
+    const uint32_t lo = __builtin_amdgcn_udot4(nz[1], 0x80402010u, __builtin_amdgcn_udot4(nz[0], 0x08040201u, 0u, false), false);
+    const uint32_t hi = __builtin_amdgcn_udot4(nz[3], 0x80402010u, __builtin_amdgcn_udot4(nz[2], 0x08040201u, 0u, false), false);
+    return (lo >> 7) | (hi << 1);  // each sum is 128 x (8-bit mask)
 }
 
 // ---- composite segment map for the single tile look-back -------------------
@@ -337,6 +346,7 @@ __global__ __launch_bounds__(T) void rl_encode_kernel(
     const uint8_t *my = img + o;
     FLRL_RL_PHASE_BEGIN();
     const uint32_t tile = take_ticket(ctrl, s_ticket);
+    FLRL_RL_TRACE(tile, 0);
     const uint64_t tile_off = (uint64_t)tile * (SUB * TB);
     const uint32_t tile_len = (uint32_t)(n - tile_off < (uint64_t)(SUB * TB) ? n - tile_off : SUB * TB);
 
@@ -375,28 +385,31 @@ __global__ __launch_bounds__(T) void rl_encode_kernel(
         L.vbl = lane_off >= n ? 0u : (n - lane_off >= LB ? (uint32_t)LB : (uint32_t)(n - lane_off));
         const uint32_t pstart = (tid == 0 && L.off > 0) ? in[L.off - 1] : 0u;
         __syncthreads();  // waits for the LDS-DMA too
+        FLRL_RL_TRACE(tile, 1 + s);
         L.p0 = row == 0 ? pstart : img[(row - 1) * LB + ((7u ^ ((row - 1) & 7u)) * 16) + 15];
-        L.ncnt = 0;
-        L.fpos = LB;
-        L.lpos = 0;
-        uint32_t p = L.p0;
+        {
+            uint32_t p = L.p0;
+            const bool full = L.off + TB <= n;  // tile-uniform: no per-chunk length masks
 #pragma unroll
-        for (int c = 0; c < CH; ++c) {
-            const u32x4 x = *reinterpret_cast<const u32x4 *>(my + ((c ^ (row & 7u)) * 16));
-            const uint32_t vb = L.vbl > 16u * c ? (L.vbl - 16u * c >= 16 ? 16u : L.vbl - 16u * c) : 0u;
-            uint32_t m = nat_mask(x, p) & (vb >= 16 ? 0xFFFFu : ((1u << vb) - 1u));
-            if (c == 0 && lane_off == 0)
-                m |= 1u;
-            if (c & 1)
-                L.nat[c / 2] |= m << 16;
-            else
-                L.nat[c / 2] = m;
-            p = x.w >> 24;
-            L.ncnt += __popc(m);
-            if (m) {
-                L.fpos = L.fpos == (uint32_t)LB ? 16u * c + (__ffs(m) - 1) : L.fpos;
-                L.lpos = 16u * c + (31u - __clz(m));
+            for (int c = 0; c < CH; ++c) {
+                const u32x4 x = *reinterpret_cast<const u32x4 *>(my + ((c ^ (row & 7u)) * 16));
+                uint32_t m = nat_mask(x, p);
+                if (!full) {
+                    const uint32_t vb = L.vbl > 16u * c ? (L.vbl - 16u * c >= 16 ? 16u : L.vbl - 16u * c) : 0u;
+                    m &= vb >= 16 ? 0xFFFFu : ((1u << vb) - 1u);
+                }
+                if (c & 1)
+                    L.nat[c / 2] |= m << 16;
+                else
+                    L.nat[c / 2] = m;
+                p = x.w >> 24;
             }
+            if (lane_off == 0)
+                L.nat[0] |= 1u;  // byte 0 is a head
+            const uint64_t a = ((uint64_t)L.nat[1] << 32) | L.nat[0], b = ((uint64_t)L.nat[3] << 32) | L.nat[2];
+            L.ncnt = (uint32_t)(__popcll(a) + __popcll(b));
+            L.fpos = a ? (uint32_t)__builtin_ctzll(a) : (b ? 64u + (uint32_t)__builtin_ctzll(b) : (uint32_t)LB);
+            L.lpos = b ? 127u - (uint32_t)__builtin_clzll(b) : (a ? 63u - (uint32_t)__builtin_clzll(a) : 0u);
         }
         const bool has = L.ncnt != 0;
         const uint32_t lmap = has ? pm_make(true, L.vbl - L.lpos) : pm_make(false, L.vbl);
@@ -510,21 +523,27 @@ __global__ __launch_bounds__(T) void rl_encode_kernel(
             ks += s_wh[v];
         }
         staged = staged && K + ks <= (uint32_t)SC;  // tile-uniform
-        if (staged && indep)
-            lane_runs(L, h0, h1, cr, tsc, tsv, K + wave_hbase + (hincl - indep));
+        const uint32_t slot = K + wave_hbase + (hincl - indep);
         if (!seen && L.sfirst != 0xFFFFFFFFu)
             first = (uint32_t)s * TB + L.sfirst;
         K += ks;
         rel_in = pm_compose(rel_in, L.smap);
+        if (w == 0 && (s + 1 == SUB || tile_off + (uint64_t)(s + 1) * TB >= n)) {
+            // the tile's map is complete: publish it before staging the last runs
+            publish_seg(status, tile, first != 0xFFFFFFFFu ? sm_nat(first, K, rel_in & 0xFFu) : sm_nonat(tile_len));
+            FLRL_RL_TRACE(tile, 3);
+        }
+        if (staged && indep)
+            lane_runs(L, h0, h1, cr, tsc, tsv, slot);
     }
     const uint32_t pre = first != 0xFFFFFFFFu ? first : tile_len;
-    const uint64_t tmap = first != 0xFFFFFFFFu ? sm_nat(first, K, rel_in & 0xFFu) : sm_nonat(tile_len);
     FLRL_RL_PHASE(1);
 
     // ---- one look-back: (heads before the tile, chunk state at its start) --
     if (w == 0) {
-        publish_seg(status, tile, tmap);
+        const uint64_t tmap = first != 0xFFFFFFFFu ? sm_nat(first, K, rel_in & 0xFFu) : sm_nonat(tile_len);
         const uint64_t state = lookback_seg<kRlLookG>(status, tile, tmap, ctrl);
+        FLRL_RL_TRACE(tile, 4);
         if (lane == 0)
             *s_state = state;
     }
@@ -645,6 +664,7 @@ __global__ __launch_bounds__(T) void rl_encode_kernel(
     }
     FLRL_RL_PHASE(3);
     FLRL_RL_PHASE_END();
+    FLRL_RL_TRACE(tile, 5);
 
     // ---- the final run (ends at byte n-1) ----------------------------------
     if (tile + 1 == ntiles && tid == 0) {
@@ -937,8 +957,8 @@ extern "C" int flrl_rl_encode_device(const uint8_t *d_in, size_t n, uint8_t *d_c
         return set_error(FLRL_E_ARG, "flrl_rl_encode_device: input too large");
     Ctrl *ctrl = static_cast<Ctrl *>(d_scratch);
     uint64_t *status = reinterpret_cast<uint64_t *>(ctrl + 1);
-    hipLaunchKernelGGL((rl_encode_kernel<kRlThreads, kRlLaneBytes, kRlSub>), dim3((uint32_t)L.tiles), dim3(kRlThreads), 0, s,
-                       d_in, (uint64_t)n, (uint32_t)L.tiles, d_counts, d_values, d_runs, ctrl, status);
+    hipLaunchKernelGGL((rl_encode_kernel<kRlThreads, kRlLaneBytes, kRlSub>), dim3((uint32_t)L.tiles), dim3(kRlThreads),
+                       FLRL_RL_DYN_LDS, s, d_in, (uint64_t)n, (uint32_t)L.tiles, d_counts, d_values, d_runs, ctrl, status);
     FLRL_HIP(hipGetLastError());
     return FLRL_OK;
 }

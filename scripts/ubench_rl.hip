@@ -38,6 +38,20 @@ __device__ __forceinline__ uint64_t rl_stamp()
 #define FLRL_RL_PHASE_END() ((void)0)
 #endif
 
+#ifdef TRACE
+__device__ uint64_t *g_trace;
+__device__ __forceinline__ uint64_t rl_rtime()
+{
+    uint64_t t;
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    return t;
+}
+#define FLRL_RL_TRACE(tile, k)                                                   \
+    do {                                                                         \
+        if (threadIdx.x == 0)                                                    \
+            g_trace[(uint64_t)(tile) * 8 + (k)] = rl_rtime(); \
+    } while (0)
+#endif
 #include "flrl_common.hip"
 #include "flrl_rl.hip"
 
@@ -73,6 +87,13 @@ int main(int argc, char **argv)
         CK(hipMemcpy(d_in, h, n, hipMemcpyHostToDevice));
         free(h);
     }
+#ifdef TRACE
+    const size_t ntiles = (n + 131071) / 131072;
+    uint64_t *d_tr;
+    CK(hipMalloc(&d_tr, ntiles * 64));
+    CK(hipMemset(d_tr, 0, ntiles * 64));
+    CK(hipMemcpyToSymbol(HIP_SYMBOL(g_trace), &d_tr, sizeof(d_tr)));
+#endif
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
@@ -132,6 +153,21 @@ int main(int argc, char **argv)
         free(h_a);
         free(h_b);
     }
+#ifdef TRACE
+    {
+        CK(hipMemset(d_tr, 0, ntiles * 64));
+        flrl_rl_encode_device(d_in, n, d_c, d_v, d_runs, d_scr, scr, nullptr);
+        CK(hipDeviceSynchronize());
+        uint64_t *h = (uint64_t *)malloc(ntiles * 64);
+        CK(hipMemcpy(h, d_tr, ntiles * 64, hipMemcpyDeviceToHost));
+        FILE *f = fopen("gpurun_out/rl_trace.bin", "wb");
+        if (f) {
+            fwrite(h, 64, ntiles, f);
+            fclose(f);
+        }
+        free(h);
+    }
+#endif
 #ifdef STAMP
     unsigned long long ph[64];
     CK(hipMemcpyFromSymbol(ph, HIP_SYMBOL(g_ph), sizeof(ph)));
