@@ -11,7 +11,7 @@
 // iff it is natural or c == 0, and then c becomes 1, else c = (c+1) mod 255.
 // Each head h emits the run that ENDS at h-1 (count = c before h, value =
 // x[h-1]); the tile holding byte n-1 emits the final run, so no tile needs
-// bytes of its successor. A tile is two 64 KiB sub-tiles that pass through LDS
+// bytes of its successor. A tile is four 32 KiB sub-tiles that pass through LDS
 // one after the other (LDS-DMA); each lane owns 128 contiguous bytes of a
 // sub-tile, so a lane holds at most one split head (before its first natural
 // head). Within a sub-tile two 32-bit scans suffice: a PhaseMap scan of lane
@@ -56,12 +56,12 @@
 
 namespace flrl {
 
-constexpr int kRlThreads = 512;                     // encode workgroup: 8 waves
+constexpr int kRlThreads = 256;                     // encode workgroup: 4 waves, 3 per CU
 constexpr int kRlLaneBytes = 128;                   // contiguous bytes per lane
-constexpr int kRlSub = 2;                           // sub-tiles per tile (one look-back each tile)
-constexpr int kRlTileBytes = kRlLaneBytes * kRlThreads * kRlSub;  // 2 x 64 KiB sub-tiles through LDS
+constexpr int kRlSub = 4;                           // sub-tiles per tile (one look-back each tile)
+constexpr int kRlTileBytes = kRlLaneBytes * kRlThreads * kRlSub;  // 4 x 32 KiB sub-tiles through LDS
 constexpr int kRlLookG = 1;      // look-back granules per lane (window 64 G tiles)
-constexpr int kRlStageBytes = 16256;  // LDS run staging (2 workgroups of 64 KiB tiles per CU)
+constexpr int kRlStageBytes = 16256;  // LDS run staging (48 KiB of LDS per workgroup)
 
 constexpr int kRdRuns = 4096;        // runs per decode tile
 constexpr int kRdThreads = 256;
@@ -187,7 +187,7 @@ __device__ __forceinline__ uint64_t sm_compose(uint64_t a, uint64_t b)
 // several dependent round trips to reach the last inclusive prefix (P). The
 // window is composed from its nearest P forward (per lane, then a 6-level
 // shuffle tree), this tile's P is published and the Const state at the tile
-// start returned. Composed window maps span <= 64*G tiles of <= 64 KiB, within
+// start returned. Composed window maps span <= 64*G tiles of <= 128 KiB, within
 // the 26-bit packed fields; across windows the accumulator is kept unpacked.
 __device__ __forceinline__ void publish_seg(uint64_t *status, uint32_t tile, uint64_t map)
 {
@@ -385,7 +385,7 @@ __global__ __launch_bounds__(T) void rl_encode_kernel(
         L.vbl = lane_off >= n ? 0u : (n - lane_off >= LB ? (uint32_t)LB : (uint32_t)(n - lane_off));
         const uint32_t pstart = (tid == 0 && L.off > 0) ? in[L.off - 1] : 0u;
         __syncthreads();  // waits for the LDS-DMA too
-        FLRL_RL_TRACE(tile, 1 + s);
+        FLRL_RL_TRACE(tile, s == 0 ? 1 : (s == SUB - 1 ? 2 : 7));  // 7: scratch slot
         L.p0 = row == 0 ? pstart : img[(row - 1) * LB + ((7u ^ ((row - 1) & 7u)) * 16) + 15];
         {
             uint32_t p = L.p0;

@@ -53,7 +53,7 @@ def test_empty():
 
 
 SIZES = [1, 2, 15, 16, 17, 255, 256, 257, 1023, 1024, 1025, 16383, 16384, 16385,
-         65535, 65536, 65537, 131071, 131072, 131073, 196609, 300_001, (1 << 20) + 7]
+         32767, 32768, 32769, 65535, 65536, 65537, 98303, 98304, 98305, 131071, 131072, 131073, 196609, 300_001, (1 << 20) + 7]
 
 
 @pytest.mark.parametrize("n", SIZES)
@@ -63,7 +63,7 @@ def test_sizes_vs_oracle(n, kind):
 
 
 @pytest.mark.parametrize("L", [254, 255, 256, 509, 510, 511, 16384 + 3, 131072 + 255, 400_000])
-@pytest.mark.parametrize("start", [0, 1, 15, 16, 1023, 16380, 65535, 65536, 131070])
+@pytest.mark.parametrize("start", [0, 1, 15, 16, 1023, 16380, 32767, 32768, 65535, 65536, 98304, 131070])
 def test_long_run_splits(L, start):
     # one long run of 7s starting at `start` inside random data
     rng = np.random.default_rng(L + start)
@@ -90,10 +90,11 @@ def test_runs_spanning_many_tiles():
     check(np.concatenate(parts))
 
 
-@pytest.mark.parametrize("quiet", [1, 65536 - 3, 65536 + 100, 131072 + 5])
+@pytest.mark.parametrize("quiet", [1, 32768 - 3, 32768 + 100, 65536 - 3, 98304 + 7, 131072 + 5])
 def test_first_natural_head_late(quiet):
-    # no natural head for `quiet` bytes (in the first sub-tile, at the sub-tile
-    # boundary, in the second sub-tile, in the next tile), then mixed data
+    # no natural head for `quiet` bytes (in the first 32 KiB sub-tile, at and
+    # after sub-tile boundaries, in the last sub-tile, in the next tile), then
+    # mixed data
     rng = np.random.default_rng(quiet)
     a = rng.integers(0, 4, size=quiet + 300_000, dtype=np.uint8)
     a[:quiet] = 5
