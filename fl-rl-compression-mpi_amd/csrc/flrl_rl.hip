@@ -359,24 +359,45 @@ __global__ __launch_bounds__(T) void rl_encode_kernel(
         uint32_t sfirst; // first natural head in the sub-tile (0xFFFFFFFF: none)
         uint64_t off;    // sub-tile offset in the input
     };
-    auto scan_sub = [&](int s, Sub &L) {
+    constexpr int NJ = WB / 1024;  // 1 KiB wave-loads per sub-tile
+    const uint32_t swz_c = ((uint32_t)lane & 7u) ^ (((uint32_t)lane >> 3) & 7u);
+    // sub-tile s of this tile into registers, placed as the LDS-DMA places it
+    auto prefetch = [&](int s, u32x4 (&pf)[NJ]) {
+        const uint64_t wave_off = tile_off + (uint64_t)s * TB + (uint64_t)w * WB;
+        if (wave_off + WB <= n) {
+#pragma unroll
+            for (int j = 0; j < NJ; ++j)
+                pf[j] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(
+                    in + wave_off + (uint32_t)(j * 8 + lane / 8) * LB + swz_c * 16));
+        } else {
+#pragma unroll
+            for (int j = 0; j < NJ; ++j)
+                pf[j] = load16_tail(in, wave_off + (uint32_t)(j * 8 + lane / 8) * LB + swz_c * 16, n);
+        }
+    };
+    // use_pf: the sub-tile is in pf (prefetched during the previous scan), else
+    // it comes by LDS-DMA; pf_next: prefetch sub-tile s+1 once this one is in LDS
+    auto scan_sub = [&](int s, Sub &L, u32x4 (&pf)[NJ], bool use_pf, bool pf_next) {
         L.off = tile_off + (uint64_t)s * TB;
         const uint64_t wave_off = L.off + (uint64_t)w * WB;
         {
-            const uint32_t c = ((uint32_t)lane & 7u) ^ (((uint32_t)lane >> 3) & 7u);
             uint8_t *dst = img + w * WB;
-            if (wave_off + WB <= n) {
+            if (use_pf) {
 #pragma unroll
-                for (int j = 0; j < WB / 1024; ++j) {
-                    const uint8_t *src = in + wave_off + (uint32_t)(j * 8 + lane / 8) * LB + c * 16;
+                for (int j = 0; j < NJ; ++j)
+                    *reinterpret_cast<u32x4 *>(dst + j * 1024 + lane * 16) = pf[j];
+            } else if (wave_off + WB <= n) {
+#pragma unroll
+                for (int j = 0; j < NJ; ++j) {
+                    const uint8_t *src = in + wave_off + (uint32_t)(j * 8 + lane / 8) * LB + swz_c * 16;
                     __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)src,
                                                      (__attribute__((address_space(3))) void *)(dst + j * 1024),
                                                      16, 0, 0);
                 }
             } else {
 #pragma unroll
-                for (int j = 0; j < WB / 1024; ++j) {
-                    const uint64_t g = wave_off + (uint32_t)(j * 8 + lane / 8) * LB + c * 16;
+                for (int j = 0; j < NJ; ++j) {
+                    const uint64_t g = wave_off + (uint32_t)(j * 8 + lane / 8) * LB + swz_c * 16;
                     *reinterpret_cast<u32x4 *>(dst + j * 1024 + lane * 16) = load16_tail(in, g, n);
                 }
             }
@@ -386,6 +407,8 @@ __global__ __launch_bounds__(T) void rl_encode_kernel(
         const uint32_t pstart = (tid == 0 && L.off > 0) ? in[L.off - 1] : 0u;
         __syncthreads();  // waits for the LDS-DMA too
         FLRL_RL_TRACE(tile, s == 0 ? 1 : (s == SUB - 1 ? 2 : 7));  // 7: scratch slot
+        if (pf_next)
+            prefetch(s + 1, pf);  // lands while this sub-tile is scanned
         L.p0 = row == 0 ? pstart : img[(row - 1) * LB + ((7u ^ ((row - 1) & 7u)) * 16) + 15];
         {
             uint32_t p = L.p0;
@@ -482,10 +505,14 @@ __global__ __launch_bounds__(T) void rl_encode_kernel(
     };
 
     // ---- sub-tiles: stage the state-independent runs ------------------------
+    // Runs are staged while they fit; from the first sub-tile that overflows the
+    // staging area on (nst), sub-tiles are re-read after the look-back instead.
+    u32x4 pf[NJ];                      // the next sub-tile, in flight during a scan
     uint32_t rel_in = kMapIdent;       // PhaseMap from the tile start to this sub-tile
     uint32_t first = 0xFFFFFFFFu;      // the tile's first natural head (tile-relative)
-    uint32_t K = 0;                    // state-independent heads staged so far
-    bool staged = true;
+    uint32_t K = 0;                    // state-independent heads so far
+    int nst = SUB;                     // sub-tiles whose runs are all staged
+    uint32_t Kst = 0, rel_st = kMapIdent;  // K and rel_in at sub-tile nst
     uint8_t v0 = 0;                    // the tile's first byte
     for (int s = 0; s < SUB; ++s) {
         if (tile_off + (uint64_t)s * TB >= n)
@@ -493,7 +520,7 @@ __global__ __launch_bounds__(T) void rl_encode_kernel(
         if (s > 0)
             __syncthreads();  // the previous sub-tile's LDS readers are done
         Sub L;
-        scan_sub(s, L);
+        scan_sub(s, L, pf, s > 0, s + 1 < SUB && tile_off + (uint64_t)(s + 1) * TB < n);
         if (s == 0)
             v0 = img[0];
         const bool seen = first != 0xFFFFFFFFu;  // a natural head before this sub-tile
@@ -522,7 +549,12 @@ __global__ __launch_bounds__(T) void rl_encode_kernel(
             wave_hbase += v < w ? s_wh[v] : 0u;
             ks += s_wh[v];
         }
-        staged = staged && K + ks <= (uint32_t)SC;  // tile-uniform
+        if (nst == SUB && K + ks > (uint32_t)SC) {  // tile-uniform
+            nst = s;
+            Kst = K;
+            rel_st = rel_in;
+        }
+        const bool stage = nst == SUB;
         const uint32_t slot = K + wave_hbase + (hincl - indep);
         if (!seen && L.sfirst != 0xFFFFFFFFu)
             first = (uint32_t)s * TB + L.sfirst;
@@ -533,8 +565,14 @@ __global__ __launch_bounds__(T) void rl_encode_kernel(
             publish_seg(status, tile, first != 0xFFFFFFFFu ? sm_nat(first, K, rel_in & 0xFFu) : sm_nonat(tile_len));
             FLRL_RL_TRACE(tile, 3);
         }
-        if (staged && indep)
+        if (stage && indep)
             lane_runs(L, h0, h1, cr, tsc, tsv, slot);
+    }
+    const int ns = (int)((tile_len + TB - 1) / TB);  // sub-tiles in this tile
+    if (nst >= ns) {
+        nst = ns;
+        Kst = K;
+        rel_st = rel_in;
     }
     const uint32_t pre = first != 0xFFFFFFFFu ? first : tile_len;
     FLRL_RL_PHASE(1);
@@ -552,37 +590,39 @@ __global__ __launch_bounds__(T) void rl_encode_kernel(
     const uint64_t h_in = sm_h(*s_state);
     const uint32_t c_in = sm_c(*s_state);
     const uint32_t S = splits(c_in, pre);  // split heads before the first natural head
-    if (staged) {
-        // split heads h_in + s end full 255-byte chunks of the tile's first byte
-        for (uint32_t j = (uint32_t)tid; j < S; j += T) {
+    {
+        // staged sub-tiles [0, nst): split heads h_in + j end full 255-byte
+        // chunks of the tile's first byte, then the staged records
+        const uint32_t st_len = (uint32_t)nst * TB;
+        const uint32_t S_st = splits(c_in, pre < st_len ? pre : st_len);
+        for (uint32_t j = (uint32_t)tid; j < S_st; j += T) {
             const uint64_t gi = h_in + j;
             if (gi > 0) {
                 counts[gi - 1] = 255;
                 values[gi - 1] = v0;
             }
         }
-        const uint64_t g0 = h_in + S;  // global index of the first natural head
-        if (K) {
+        const uint64_t g0 = h_in + S_st;  // global index of the first natural head
+        if (Kst) {
             if (tid == 0 && g0 > 0) {
                 const uint32_t c = add_c(c_in, first);
                 counts[g0 - 1] = (uint8_t)(c == 0 ? 255u : c);
                 values[g0 - 1] = tsv[0];
             }
-            for (uint32_t j = 1 + (uint32_t)tid; j < K; j += T) {
+            for (uint32_t j = 1 + (uint32_t)tid; j < Kst; j += T) {
                 counts[g0 + j - 1] = tsc[j];
                 values[g0 + j - 1] = tsv[j];
             }
         }
-    } else {
-        // dense tile: re-read each sub-tile and emit with the true states
-        uint32_t rel = kMapIdent;
-        uint64_t hb = h_in;  // heads before the sub-tile
-        for (int s = 0; s < SUB; ++s) {
-            if (tile_off + (uint64_t)s * TB >= n)
-                break;
-            __syncthreads();
+    }
+    if (nst < ns) {
+        // sub-tiles [nst, ns): re-read and emit with the true states
+        uint32_t rel = rel_st;
+        uint64_t hb = h_in + splits(c_in, pre < (uint32_t)nst * TB ? pre : (uint32_t)nst * TB) + Kst;
+        for (int s = nst; s < ns; ++s) {
+            __syncthreads();  // staging and image readers are done
             Sub L;
-            scan_sub(s, L);
+            scan_sub(s, L, pf, s > nst, s + 1 < ns);
             const uint32_t c_lane = pm_apply(pm_compose(rel, L.lrel), c_in);
             uint64_t hm0, hm1;
             head_masks(L, c_lane, true, hm0, hm1);

@@ -2,7 +2,7 @@
 // (the product kernel itself, compiled in with its phase hooks enabled).
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 [-DSTAMP] -I include \
 //         -I fl-rl-compression-mpi_amd/csrc scripts/ubench_rl.hip -o scripts/ubench_rl.bin
-//   scripts/ubench_rl.bin [kind=2(runs32)] [n=1 GiB] [reps=20]
+//   scripts/ubench_rl.bin [kind=3 (runs32); 100+M: runs of 1..M] [n=1 GiB] [reps=20]
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -80,7 +80,18 @@ int main(int argc, char **argv)
     CK(hipMalloc(&d_scr, scr));
     {
         uint8_t *h = (uint8_t *)malloc(n);
-        if (flrl_gen_host(kind, 42, 0, h, n) != FLRL_OK) {
+        if (kind >= 100) {  // runs of 1..(kind-100) bytes, fresh value per run
+            const uint32_t maxrun = (uint32_t)(kind - 100);
+            uint64_t x = 88172645463325252ull;
+            uint8_t v = 0;
+            for (size_t i = 0; i < n;) {
+                x ^= x << 13, x ^= x >> 7, x ^= x << 17;
+                size_t L = 1 + (size_t)(x % maxrun);
+                v = (uint8_t)(v + 1 + (x >> 32) % 254);
+                for (size_t k = 0; k < L && i < n; ++k)
+                    h[i++] = v;
+            }
+        } else if (flrl_gen_host(kind, 42, 0, h, n) != FLRL_OK) {
             fprintf(stderr, "gen: %s\n", flrl_last_error());
             return 1;
         }

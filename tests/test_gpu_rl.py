@@ -102,10 +102,11 @@ def test_first_natural_head_late(quiet):
     check(a)
 
 
-@pytest.mark.parametrize("maxrun", [6, 12, 20, 40])
+@pytest.mark.parametrize("maxrun", [6, 12, 20, 28, 40])
 def test_medium_density(maxrun):
     # mean runs around the staging threshold (state-independent runs per tile
-    # vs the LDS staging capacity): both emission paths, mixed per tile
+    # vs the LDS staging capacity): the staging overflows in the first, second,
+    # third or last 32 KiB sub-tile of a tile, or not at all
     rng = np.random.default_rng(maxrun)
     lens = rng.integers(1, maxrun + 1, size=400_000)
     vals = (np.cumsum(rng.integers(1, 255, size=lens.size)) % 256).astype(np.uint8)
