@@ -257,6 +257,55 @@ __device__ __forceinline__ uint64_t lookback_sum(uint64_t *status, uint32_t tile
     return lookback_resolve(status, tile, agg, ctrl);
 }
 
+// Exclusive prefix of per-workgroup aggregates for the pre-pass scans: the
+// whole T-thread workgroup publishes its aggregate and then reads EVERY
+// predecessor's (4 per thread per round, all loads in flight together), so the
+// prefix costs one round trip once they are published instead of a chain of
+// look-back windows, each waiting for an inclusive prefix further back. For
+// grids of at most kMaxPrefixBlocks workgroups, taken in ticket order (so each
+// predecessor is running or done). s_red: T/64 words of LDS.
+constexpr uint32_t kMaxPrefixBlocks = 1024;
+template <int T>
+__device__ __forceinline__ uint64_t block_prefix_all(uint64_t *status, uint32_t blk, uint64_t agg,
+                                                     Ctrl *ctrl, uint64_t *s_red)
+{
+    const int tid = threadIdx.x;
+    if (tid == 0)
+        granule_store(&status[blk], kFlagA | agg);
+    uint64_t sum = 0;
+    for (uint32_t j0 = 0; j0 < blk; j0 += 4 * T) {
+        uint64_t g[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t j = j0 + (uint32_t)tid + (uint32_t)k * T;
+            g[k] = j < blk ? granule_load(&status[j]) : kFlagA;
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t j = j0 + (uint32_t)tid + (uint32_t)k * T;
+            uint32_t spins = 0;
+            while ((g[k] >> 62) == 0) {
+                if (++spins > kSpinLimit) {
+                    raise_error(ctrl, FLRL_E_TIMEOUT);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+                g[k] = granule_load(&status[j]);
+            }
+            sum += g[k] & kPayload;
+        }
+    }
+    sum = wave_sum_u64(sum);
+    if ((tid & (kWave - 1)) == 0)
+        s_red[tid / kWave] = sum;
+    __syncthreads();
+    uint64_t excl = 0;
+#pragma unroll
+    for (int v = 0; v < T / kWave; ++v)
+        excl += s_red[v];
+    return excl;
+}
+
 // 16-byte load of bytes [o, o+16) of p (o and p 16-byte aligned), zero-filling
 // past n. A straddling chunk is read whole: a 16-byte-aligned block never
 // crosses a page, so this cannot fault; the bytes at or past n are masked off.

@@ -297,88 +297,100 @@ __global__ __launch_bounds__(T, 1) void fl_encode_kernel(
     }
 }
 
-// Decode pre-pass: one workgroup scans kOffFrames frame widths (64 per lane),
-// validates them (a width outside [1,8] raises FLRL_E_FORMAT and is clamped, as
-// fl_decode_kernel clamps it, so offsets stay consistent and in bounds), and
-// writes the output offset (16-byte units) of each 256-frame decode tile:
-// tile_base[t] for t < ntiles and tile_base[ntiles] = total. Workgroup offsets
-// come from a decoupled look-back; the workgroup holding the last frame checks
-// valuesSize against the widths.
+// Decode pre-pass: one workgroup scans `iters` x kOffFrames frame widths (64
+// per lane per round), validates them (a width outside [1,8] raises
+// FLRL_E_FORMAT and is clamped, as fl_decode_kernel clamps it, so offsets stay
+// consistent and in bounds), and writes the output offset (16-byte units) of
+// each 256-frame decode tile: tile_base[t] for t < ntiles and tile_base[ntiles]
+// = total. Offsets are first written workgroup-relative; once the workgroup's
+// base is known (block_prefix_all: iters keeps the grid within
+// kMaxPrefixBlocks) each lane adds it to the entries it wrote. The workgroup
+// holding the last frame checks valuesSize against the widths.
 __global__ __launch_bounds__(kThreads) void fl_offsets_kernel(
     const uint8_t *__restrict__ bits, uint64_t nframes, uint64_t vsize, uint64_t n,
-    uint64_t *__restrict__ tile_base, uint32_t ntiles, uint32_t nblocks, Ctrl *ctrl,
+    uint64_t *__restrict__ tile_base, uint32_t ntiles, uint32_t nblocks, uint32_t iters, Ctrl *ctrl,
     uint64_t *status)
 {
     __shared__ uint32_t s_wave[kWaves];
     __shared__ uint32_t s_ticket;
-    __shared__ uint64_t s_base;
+    __shared__ uint64_t s_red[kWaves];
     const int tid = threadIdx.x;
     const int lane = tid & (kWave - 1);
     const int wave = tid / kWave;
     const uint32_t blk = take_ticket(ctrl, &s_ticket);
-    const uint64_t f0 = (uint64_t)blk * kOffFrames + (uint64_t)tid * kOffFramesPerThread;
-
-    // widths 4 per dword (SWAR): a byte is invalid if it is 0 or > 8
-    uint32_t sum = 0;
+    uint64_t local = 0;          // frames' 16-byte units before this round, workgroup-relative
+    bool has_last = false;       // this lane holds the last frame
+    uint64_t last_local = 0;     // its units before the last frame, workgroup-relative
     bool bad = false;
+    for (uint32_t it = 0; it < iters; ++it) {
+        const uint64_t f0 = ((uint64_t)blk * iters + it) * kOffFrames + (uint64_t)tid * kOffFramesPerThread;
+        // widths 4 per dword (SWAR): a byte is invalid if it is 0 or > 8
+        uint32_t sum = 0;
 #pragma unroll
-    for (int q = 0; q < kOffFramesPerThread / 16; ++q) {
-        const uint64_t fq = f0 + 16 * q;
-        if (fq + 16 <= nframes) {
-            const u32x4 w = *reinterpret_cast<const u32x4 *>(bits + fq);
+        for (int q = 0; q < kOffFramesPerThread / 16; ++q) {
+            const uint64_t fq = f0 + 16 * q;
+            if (fq + 16 <= nframes) {
+                const u32x4 w = *reinterpret_cast<const u32x4 *>(bits + fq);
 #pragma unroll
-            for (int d = 0; d < 4; ++d) {
-                const uint32_t x = w[d];
-                const uint32_t zero = (x - 0x01010101u) & ~x & 0x80808080u;
-                const uint32_t big = (((x & 0x7F7F7F7Fu) + 0x77777777u) | x) & 0x80808080u;
-                if (zero | big) {  // rare: clamp byte by byte
-                    bad = true;
-                    for (int i = 0; i < 4; ++i)
-                        sum += clamp_width((x >> (8 * i)) & 0xFFu);
-                } else {
-                    const uint32_t h = (x & 0x00FF00FFu) + ((x >> 8) & 0x00FF00FFu);
-                    sum += (h & 0xFFFFu) + (h >> 16);
+                for (int d = 0; d < 4; ++d) {
+                    const uint32_t x = w[d];
+                    const uint32_t zero = (x - 0x01010101u) & ~x & 0x80808080u;
+                    const uint32_t big = (((x & 0x7F7F7F7Fu) + 0x77777777u) | x) & 0x80808080u;
+                    if (zero | big) {  // rare: clamp byte by byte
+                        bad = true;
+                        for (int i = 0; i < 4; ++i)
+                            sum += clamp_width((x >> (8 * i)) & 0xFFu);
+                    } else {
+                        const uint32_t h = (x & 0x00FF00FFu) + ((x >> 8) & 0x00FF00FFu);
+                        sum += (h & 0xFFFFu) + (h >> 16);
+                    }
+                }
+            } else {
+                for (int i = 0; i < 16 && fq + i < nframes; ++i) {
+                    const uint32_t raw = bits[fq + i];
+                    bad |= raw < 1 || raw > 8;
+                    sum += clamp_width(raw);
                 }
             }
-        } else {
-            for (int i = 0; i < 16 && fq + i < nframes; ++i) {
-                const uint32_t raw = bits[fq + i];
-                bad |= raw < 1 || raw > 8;
-                sum += clamp_width(raw);
-            }
         }
+        // exclusive scan of lane sums over the workgroup
+        const uint32_t inc = wave_incl_scan_u32(sum);
+        if (it > 0)
+            __syncthreads();  // the previous round's s_wave readers are done
+        if (lane == kWave - 1)
+            s_wave[wave] = inc;
+        __syncthreads();
+        uint32_t before = 0, agg = 0;
+#pragma unroll
+        for (int w = 0; w < kWaves; ++w) {
+            before += w < wave ? s_wave[w] : 0u;
+            agg += s_wave[w];
+        }
+        const uint32_t excl = before + inc - sum;
+        const uint64_t tile = f0 / kDecTileFrames;
+        if ((tid & 3) == 0 && tile < ntiles)
+            tile_base[tile] = local + excl;
+        if (nframes > f0 && nframes <= f0 + kOffFramesPerThread) {
+            has_last = true;
+            last_local = local + excl + sum - clamp_width(bits[nframes - 1]);
+        }
+        local += agg;
     }
     if (bad)
         raise_error(ctrl, FLRL_E_FORMAT);
-
-    // exclusive scan of lane sums over the workgroup
-    const uint32_t inc = wave_incl_scan_u32(sum);
-    if (lane == kWave - 1)
-        s_wave[wave] = inc;
-    __syncthreads();
-    uint32_t before = 0, agg = 0;
-#pragma unroll
-    for (int w = 0; w < kWaves; ++w) {
-        before += w < wave ? s_wave[w] : 0u;
-        agg += s_wave[w];
+    const uint64_t base = block_prefix_all<kThreads>(status, blk, local, ctrl, s_red);
+    for (uint32_t it = 0; it < iters; ++it) {
+        const uint64_t f0 = ((uint64_t)blk * iters + it) * kOffFrames + (uint64_t)tid * kOffFramesPerThread;
+        const uint64_t tile = f0 / kDecTileFrames;
+        if ((tid & 3) == 0 && tile < ntiles)
+            tile_base[tile] += base;  // this lane's own entry
     }
-    const uint32_t excl = before + inc - sum;
-    if (wave == 0) {
-        const uint64_t e = lookback_sum(status, blk, agg, ctrl);
-        if (tid == 0)
-            s_base = e;
-    }
-    __syncthreads();
-    const uint64_t base = s_base;
-    const uint64_t tile = f0 / kDecTileFrames;
-    if ((tid & 3) == 0 && tile < ntiles)
-        tile_base[tile] = base + excl;
     if (blk + 1 == nblocks && tid == 0)
-        tile_base[ntiles] = base + agg;
-    if (nframes > f0 && nframes <= f0 + kOffFramesPerThread) {  // this lane holds the last frame
+        tile_base[ntiles] = base + local;
+    if (has_last) {
         const uint32_t b_last = clamp_width(bits[nframes - 1]);
         const uint64_t cnt = n - (nframes - 1) * kFrame;
-        const uint64_t expect = 16ull * (base + excl + sum - b_last) + (cnt * b_last + 7) / 8;
+        const uint64_t expect = 16ull * (base + last_local) + (cnt * b_last + 7) / 8;
         if (expect != vsize)
             raise_error(ctrl, FLRL_E_FORMAT);
     }
@@ -467,14 +479,17 @@ __global__ __launch_bounds__(kThreads) void fl_decode_kernel(
 // [Ctrl 16 B][decode: status[off_blocks] (16-B padded)][tile_base[dec_tiles + 1]]
 // Only Ctrl + status are zeroed per call.
 struct FlLayout {
-    size_t enc_tiles, dec_tiles, off_blocks;
+    size_t enc_tiles, dec_tiles, off_blocks, off_iters;
     size_t enc_zero, dec_zero, bytes;
     explicit FlLayout(size_t n)
     {
         const size_t frames = div_up(n, kFrame);
         enc_tiles = div_up(n, (size_t)kEncTileBytes);
         dec_tiles = div_up(n, (size_t)kDecTileBytes);
-        off_blocks = div_up(frames, (size_t)kOffFrames);
+        // offsets rounds per workgroup: the grid stays within kMaxPrefixBlocks
+        off_iters = div_up(div_up(frames, (size_t)kOffFrames), (size_t)kMaxPrefixBlocks);
+        off_iters = off_iters ? off_iters : 1;
+        off_blocks = div_up(frames, (size_t)kOffFrames * off_iters);
         enc_zero = sizeof(Ctrl) + round_up(enc_tiles * 8, 16);
         dec_zero = sizeof(Ctrl) + round_up(off_blocks * 8, 16);
         const size_t dec_bytes = dec_zero + round_up((dec_tiles + 1) * 8, 16);
@@ -559,7 +574,7 @@ extern "C" int flrl_fl_decode_device(const uint8_t *d_bits, size_t bits_size,
         reinterpret_cast<uint64_t *>(static_cast<uint8_t *>(d_scratch) + L.dec_zero);
     hipLaunchKernelGGL(fl_offsets_kernel, dim3((uint32_t)L.off_blocks), dim3(kThreads), 0, s,
                        d_bits, (uint64_t)bits_size, (uint64_t)values_size, (uint64_t)n, tile_base,
-                       (uint32_t)L.dec_tiles, (uint32_t)L.off_blocks, ctrl, status);
+                       (uint32_t)L.dec_tiles, (uint32_t)L.off_blocks, (uint32_t)L.off_iters, ctrl, status);
     FLRL_HIP(hipGetLastError());
     hipLaunchKernelGGL(fl_decode_kernel<kDecItems>, dim3((uint32_t)L.dec_tiles), dim3(kThreads), 0,
                        s, d_bits, (uint64_t)bits_size, d_values, (uint64_t)values_size, d_out,

@@ -717,65 +717,72 @@ __global__ __launch_bounds__(T) void rl_encode_kernel(
 }
 
 // ---- decode pre-pass: output offsets of each decode tile ------------------
+// `iters` rounds of kRoRuns counts per workgroup; offsets are written
+// workgroup-relative, then the workgroup's base (block_prefix_all) is added.
 __global__ __launch_bounds__(kThreads) void rl_offsets_kernel(
     const uint8_t *__restrict__ counts, uint64_t runs, uint64_t n, uint64_t *__restrict__ tile_base,
-    uint32_t ntiles, uint32_t nblocks, Ctrl *ctrl, uint64_t *status)
+    uint32_t ntiles, uint32_t nblocks, uint32_t iters, Ctrl *ctrl, uint64_t *status)
 {
     __shared__ uint32_t s_wave[kWaves];
     __shared__ uint32_t s_ticket;
-    __shared__ uint64_t s_base;
+    __shared__ uint64_t s_red[kWaves];
     const int tid = threadIdx.x;
     const int lane = tid & (kWave - 1);
     const int wave = tid / kWave;
     const uint32_t blk = take_ticket(ctrl, &s_ticket);
-    const uint64_t r0 = (uint64_t)blk * kRoRuns + (uint64_t)tid * kRoRunsPerThread;
-
-    uint32_t sum = 0;
+    constexpr int kLanesPerTile = kRdRuns / kRoRunsPerThread;
+    uint64_t local = 0;  // output bytes before this round, workgroup-relative
     bool bad = false;
+    for (uint32_t it = 0; it < iters; ++it) {
+        const uint64_t r0 = ((uint64_t)blk * iters + it) * kRoRuns + (uint64_t)tid * kRoRunsPerThread;
+        uint32_t sum = 0;
 #pragma unroll 4
-    for (int q = 0; q < kRoRunsPerThread / 16; ++q) {
-        const uint64_t rq = r0 + 16 * q;
-        const u32x4 v = load16_tail(counts, rq, runs);
+        for (int q = 0; q < kRoRunsPerThread / 16; ++q) {
+            const uint64_t rq = r0 + 16 * q;
+            const u32x4 v = load16_tail(counts, rq, runs);
 #pragma unroll
-        for (int d = 0; d < 4; ++d) {
-            const uint32_t x = v[d];
-            const uint32_t h = (x & 0x00FF00FFu) + ((x >> 8) & 0x00FF00FFu);
-            sum += (h & 0xFFFFu) + (h >> 16);
-            // a zero count inside [0, runs) is malformed
-            const uint32_t zero = (x - 0x01010101u) & ~x & 0x80808080u;
-            if (zero) {
-                for (int i = 0; i < 4; ++i)
-                    bad |= rq + 4 * d + i < runs && ((x >> (8 * i)) & 0xFFu) == 0;
+            for (int d = 0; d < 4; ++d) {
+                const uint32_t x = v[d];
+                const uint32_t h = (x & 0x00FF00FFu) + ((x >> 8) & 0x00FF00FFu);
+                sum += (h & 0xFFFFu) + (h >> 16);
+                // a zero count inside [0, runs) is malformed
+                const uint32_t zero = (x - 0x01010101u) & ~x & 0x80808080u;
+                if (zero) {
+                    for (int i = 0; i < 4; ++i)
+                        bad |= rq + 4 * d + i < runs && ((x >> (8 * i)) & 0xFFu) == 0;
+                }
             }
         }
+        const uint32_t inc = wave_incl_scan_u32(sum);
+        if (it > 0)
+            __syncthreads();  // the previous round's s_wave readers are done
+        if (lane == kWave - 1)
+            s_wave[wave] = inc;
+        __syncthreads();
+        uint32_t before = 0, agg = 0;
+#pragma unroll
+        for (int v = 0; v < kWaves; ++v) {
+            before += v < wave ? s_wave[v] : 0u;
+            agg += s_wave[v];
+        }
+        const uint64_t tile = r0 / kRdRuns;
+        if (tid % kLanesPerTile == 0 && tile < ntiles)
+            tile_base[tile] = local + before + inc - sum;
+        local += agg;
     }
     if (bad)
         raise_error(ctrl, FLRL_E_FORMAT);
-    const uint32_t inc = wave_incl_scan_u32(sum);
-    if (lane == kWave - 1)
-        s_wave[wave] = inc;
-    __syncthreads();
-    uint32_t before = 0, agg = 0;
-#pragma unroll
-    for (int v = 0; v < kWaves; ++v) {
-        before += v < wave ? s_wave[v] : 0u;
-        agg += s_wave[v];
+    // workgroup base from all predecessors (iters keeps the grid within kMaxPrefixBlocks)
+    const uint64_t base = block_prefix_all<kThreads>(status, blk, local, ctrl, s_red);
+    for (uint32_t it = 0; it < iters; ++it) {
+        const uint64_t r0 = ((uint64_t)blk * iters + it) * kRoRuns + (uint64_t)tid * kRoRunsPerThread;
+        const uint64_t tile = r0 / kRdRuns;
+        if (tid % kLanesPerTile == 0 && tile < ntiles)
+            tile_base[tile] += base;  // this lane's own entry
     }
-    const uint32_t excl = before + inc - sum;
-    if (wave == 0) {
-        const uint64_t e = lookback_sum(status, blk, agg, ctrl);
-        if (tid == 0)
-            s_base = e;
-    }
-    __syncthreads();
-    const uint64_t base = s_base;
-    constexpr int kLanesPerTile = kRdRuns / kRoRunsPerThread;
-    const uint64_t tile = r0 / kRdRuns;
-    if (tid % kLanesPerTile == 0 && tile < ntiles)
-        tile_base[tile] = base + excl;
     if (blk + 1 == nblocks && tid == 0) {
-        tile_base[ntiles] = base + agg;
-        if (base + agg != n)
+        tile_base[ntiles] = base + local;
+        if (base + local != n)
             raise_error(ctrl, FLRL_E_FORMAT);
     }
 }
@@ -954,11 +961,14 @@ struct RlEncLayout {
 };
 
 struct RlDecLayout {
-    size_t tiles, blocks, zero, bytes;
+    size_t tiles, blocks, iters, zero, bytes;
     explicit RlDecLayout(size_t runs)
     {
         tiles = div_up(runs, (size_t)kRdRuns);
-        blocks = div_up(runs, (size_t)kRoRuns);
+        // offsets rounds per workgroup: the grid stays within kMaxPrefixBlocks
+        iters = div_up(div_up(runs, (size_t)kRoRuns), (size_t)kMaxPrefixBlocks);
+        iters = iters ? iters : 1;
+        blocks = div_up(runs, (size_t)kRoRuns * iters);
         zero = sizeof(Ctrl) + round_up(blocks * 8, 16);
         bytes = zero + round_up((tiles + 1) * 8, 16);
     }
@@ -1038,7 +1048,7 @@ extern "C" int flrl_rl_decode_device(const uint8_t *d_counts, const uint8_t *d_v
         reinterpret_cast<uint64_t *>(static_cast<uint8_t *>(d_scratch) + L.zero);
     hipLaunchKernelGGL(rl_offsets_kernel, dim3((uint32_t)L.blocks), dim3(kThreads), 0, s, d_counts,
                        (uint64_t)runs, (uint64_t)n, tile_base, (uint32_t)L.tiles,
-                       (uint32_t)L.blocks, ctrl, status);
+                       (uint32_t)L.blocks, (uint32_t)L.iters, ctrl, status);
     FLRL_HIP(hipGetLastError());
     const size_t rgrid = (size_t)kRdPerCU * (size_t)cu_count();
     hipLaunchKernelGGL(rl_decode_kernel, dim3((uint32_t)(L.tiles < rgrid ? L.tiles : rgrid)), dim3(kRdThreads), 0,

@@ -233,6 +233,25 @@ def test_device_16gib_lo4_shard_equivalence():
     torch.cuda.empty_cache()
 
 
+def test_device_decode_offsets_rounds():
+    """A ragged 2 GiB input: more than 1024 x 16384 frames, so the decode
+    pre-pass runs two rounds per workgroup with a partial last workgroup; the
+    offsets' width sum also equals valuesSize."""
+    from flrl.device import FLDevice, gen
+    n = (2 << 30) + 12345
+    x = gen("lo4", n, 5)
+    x[n - 1] = 0xFF  # a full-width last (partial) frame
+    d = FLDevice(n)
+    d.encode(x)
+    v = d.values_size()
+    assert d.error() == 0
+    out = d.decode(v)
+    assert d.error() == 0
+    assert torch.equal(out, x[:n])
+    del d, x, out
+    torch.cuda.empty_cache()
+
+
 # ------------------------------------------------------------------ sharded
 def test_sharded_equals_single(bmp_bytes):
     ng = flrl.device_count()

@@ -113,6 +113,12 @@ def test_medium_density(maxrun):
     check(np.repeat(vals, lens)[:2_000_003])
 
 
+def test_decode_offsets_rounds():
+    # random bytes: ~72M runs, more than 1024 x 65536, so the decode pre-pass
+    # runs two rounds per workgroup with a partial last workgroup
+    check(oracle.gen("u8", (72 << 20) + 999, 23))
+
+
 def test_all_zero_large():
     a = np.zeros(5 * 131072 + 77, np.uint8)  # no natural head after byte 0
     r = check(a)
