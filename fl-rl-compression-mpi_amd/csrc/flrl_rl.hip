@@ -480,10 +480,14 @@ __global__ __launch_bounds__(T) void rl_encode_kernel(
         }
     };
     // a lane's runs in order from head masks: count = distance to the previous
-    // head (the lane's first: c_first + pos), value = the byte before the head
+    // head (the lane's first: c_first + pos), value = the byte before the head.
+    // No natural head lies strictly between two heads, so that byte equals the
+    // byte AT the previous head (the lane's first run: the byte before the
+    // lane, p0): it is read one iteration ahead, off the loop's critical path.
     auto lane_runs = [&](const Sub &L, uint64_t h0, uint64_t h1, uint32_t c_first, uint8_t *sc, uint8_t *sv,
                          uint32_t slot) {
         int prev = -1;
+        uint32_t val = L.p0;
         while (h0 | h1) {
             int pos;
             if (h0) {
@@ -495,10 +499,11 @@ __global__ __launch_bounds__(T) void rl_encode_kernel(
             }
             uint32_t cnt = prev < 0 ? add_c(c_first, (uint32_t)pos) : (uint32_t)(pos - prev);
             cnt = cnt == 0 ? 255u : cnt;
-            const uint32_t q = (uint32_t)pos - 1;
-            const uint32_t val = pos == 0 ? L.p0 : my[(((q >> 4) ^ (row & 7u)) * 16) + (q & 15u)];
+            const uint32_t q = (uint32_t)pos;
+            const uint32_t nval = my[(((q >> 4) ^ (row & 7u)) * 16) + (q & 15u)];  // the next run's value
             sc[slot] = (uint8_t)cnt;
             sv[slot] = (uint8_t)val;
+            val = nval;
             ++slot;
             prev = pos;
         }
