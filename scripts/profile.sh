@@ -11,16 +11,17 @@ export TMPDIR=/tmp
 TAG=${1:-r01}
 shift
 BENCH_ARGS=("$@")
-[ ${#BENCH_ARGS[@]} -eq 0 ] && BENCH_ARGS=(--steps 20 --warmup 5 --cpu-sample 0)
+# the 16 GiB north-star launches would mix into the 1 GiB kernel averages: profile them separately
+[ ${#BENCH_ARGS[@]} -eq 0 ] && BENCH_ARGS=(--no-north-star)
 OUT=gpurun_out/prof/$TAG
 mkdir -p "$OUT"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run \
-    -- python3 bench.py "${BENCH_ARGS[@]}" > "$OUT/trace.log" 2>&1 || { echo "trace pass failed"; tail -20 "$OUT/trace.log"; exit 1; }
+    -- python3 bench.py --steps 20 --warmup 5 --cpu-sample 0 "${BENCH_ARGS[@]}" > "$OUT/trace.log" 2>&1 || { echo "trace pass failed"; tail -20 "$OUT/trace.log"; exit 1; }
 echo "trace pass ok"
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch" -o run \
-    -- python3 bench.py --steps 3 --warmup 1 --cpu-sample 0 "${@:1}" > "$OUT/fetch.log" 2>&1 || { echo "fetch pass failed"; tail -20 "$OUT/fetch.log"; exit 1; }
+    -- python3 bench.py --steps 3 --warmup 1 --cpu-sample 0 "${BENCH_ARGS[@]}" > "$OUT/fetch.log" 2>&1 || { echo "fetch pass failed"; tail -20 "$OUT/fetch.log"; exit 1; }
 echo "fetch pass ok"
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write" -o run \
-    -- python3 bench.py --steps 3 --warmup 1 --cpu-sample 0 "${@:1}" > "$OUT/write.log" 2>&1 || { echo "write pass failed"; tail -20 "$OUT/write.log"; exit 1; }
+    -- python3 bench.py --steps 3 --warmup 1 --cpu-sample 0 "${BENCH_ARGS[@]}" > "$OUT/write.log" 2>&1 || { echo "write pass failed"; tail -20 "$OUT/write.log"; exit 1; }
 echo "write pass ok"
 find "$OUT" -name "*.csv" | head -20
