@@ -23,10 +23,11 @@
 //
 // Decode is two launches: fl_offsets_kernel scans the frame widths (F bytes,
 // <1% of the traffic) into per-tile output offsets and validates the widths
-// and valuesSize; fl_decode_kernel is then a pure streaming kernel with no
-// inter-workgroup dependency: each 32 KiB output tile loads its widths and its
-// contiguous packed bytes (16-B aligned) into LDS, unpacks 2b bytes -> 16 bytes
-// per lane and stores coalesced.
+// and valuesSize; fl_decode_kernel is then a streaming kernel with no
+// inter-workgroup dependency: persistent grid-stride workgroups take 32 KiB
+// output tiles, load each tile's widths and contiguous packed bytes (16-B
+// aligned) one tile ahead into registers, stage the bytes in LDS and unpack
+// 2b bytes -> 16 bytes per lane.
 //
 // Replaces the reference kernels compressCalculateOutputBits
 // (fl_gpu.cu:648-685), compressInitializeFrameStartIndiciesBits + thrust scan
@@ -49,12 +50,16 @@ namespace flrl {
 constexpr int kEncThreads = 512;  // encode workgroup: 8 waves, one per CU (LDS 133 KB)
 constexpr int kEncItems = 16;     // encode tile = 512 lanes x 16 x 16 B = 128 KiB (1024 frames)
 constexpr int kEncTileBytes = kEncThreads * 16 * kEncItems;
-constexpr int kDecItems = 8;   // decode tile = 32 KiB (256 frames)
-constexpr int kDecTileBytes = kThreads * 16 * kDecItems;
+constexpr int kDecThreads = 512;  // decode workgroup: 8 waves
+constexpr int kDecItems = 8;      // decode tile = 512 lanes x 8 x 16 B = 64 KiB (512 frames)
+constexpr int kDecPerCU = 2;      // persistent decode workgroups per CU (LDS 64 KiB each)
+constexpr int kDecTileBytes = kDecThreads * 16 * kDecItems;
 constexpr int kDecTileFrames = kDecTileBytes / kFrame;
 constexpr int kOffFramesPerThread = 64;
 constexpr int kOffFrames = kThreads * kOffFramesPerThread;  // frames per offsets workgroup
-static_assert(kOffFramesPerThread * 4 == kDecTileFrames, "4 offsets lanes per decode tile");
+constexpr int kOffLanesPerTile = kDecTileFrames / kOffFramesPerThread;  // offsets lanes per decode tile
+static_assert(kOffLanesPerTile * kOffFramesPerThread == kDecTileFrames && kThreads % kOffLanesPerTile == 0,
+              "a decode tile is whole offsets lanes");
 
 // Pack 8 bytes (each < 2^b) of x into the low 8b bits, value i at bit b*i.
 __device__ __forceinline__ uint64_t pack8(uint64_t x, uint32_t b)
@@ -368,7 +373,7 @@ __global__ __launch_bounds__(kThreads) void fl_offsets_kernel(
         }
         const uint32_t excl = before + inc - sum;
         const uint64_t tile = f0 / kDecTileFrames;
-        if ((tid & 3) == 0 && tile < ntiles)
+        if (tid % kOffLanesPerTile == 0 && tile < ntiles)
             tile_base[tile] = local + excl;
         if (nframes > f0 && nframes <= f0 + kOffFramesPerThread) {
             has_last = true;
@@ -382,7 +387,7 @@ __global__ __launch_bounds__(kThreads) void fl_offsets_kernel(
     for (uint32_t it = 0; it < iters; ++it) {
         const uint64_t f0 = ((uint64_t)blk * iters + it) * kOffFrames + (uint64_t)tid * kOffFramesPerThread;
         const uint64_t tile = f0 / kDecTileFrames;
-        if ((tid & 3) == 0 && tile < ntiles)
+        if (tid % kOffLanesPerTile == 0 && tile < ntiles)
             tile_base[tile] += base;  // this lane's own entry
     }
     if (blk + 1 == nblocks && tid == 0)
@@ -396,81 +401,151 @@ __global__ __launch_bounds__(kThreads) void fl_offsets_kernel(
     }
 }
 
+// Decode: persistent grid-stride workgroups (kDecPerCU per CU) over 32 KiB
+// output tiles; the packed bytes (and frame widths) of a workgroup's next tile
+// are loaded into registers right after the current tile's width scan, while
+// the current tile is unpacked from LDS. Lane group g = tid/8 owns frames
+// g*ITEMS .. +ITEMS-1 of the tile (its prefix is a register running sum after
+// one wave scan); lane tid%8 unpacks 16-byte chunk tid%8 of each. Measured
+// against the one-tile-per-workgroup form (scripts/ubench_decode.hip): -5 %
+// on 1 GiB u8 and lo4; contiguous per-workgroup tile ranges (which would let
+// the offsets pre-pass fuse into this kernel) were 20 % slower.
 template <int ITEMS>
-__global__ __launch_bounds__(kThreads) void fl_decode_kernel(
-    const uint8_t *__restrict__ bits, uint64_t nframes, const uint8_t *__restrict__ values,
-    uint64_t vsize, uint8_t *__restrict__ out, uint64_t n, const uint64_t *__restrict__ tile_base)
+__device__ __forceinline__ void dec_load_values(u32x4 (&a)[ITEMS], const uint8_t *values, uint64_t base,
+                                                uint32_t agg, uint64_t vsize)
 {
-    constexpr int TB = kThreads * 16 * ITEMS;
-    constexpr int TF = TB / kFrame;
-    __shared__ u32x4 s_in[TB / 16 + 2];  // +2: a lane may read up to 18 bytes past its frame
-    __shared__ u32x4 s_w4[TF / 16];
-    __shared__ uint32_t s_pref[TF];
-    __shared__ uint32_t s_wave[kWaves];
-    uint8_t *s_w = reinterpret_cast<uint8_t *>(s_w4);
-
     const int tid = threadIdx.x;
-    const uint64_t tile = blockIdx.x;
-    const uint64_t tile_off = tile * TB;
-    const uint64_t frame0 = tile * TF;
-    const uint64_t base = tile_base[tile];
-    const uint32_t agg = (uint32_t)(tile_base[tile + 1] - base);
-
-    // ---- issue the tile's loads: its widths and its packed bytes ---------
-    if (tid < TF / 16) {
-        u32x4 w = load16_tail(bits, frame0 + 16 * tid, nframes);
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            const uint32_t raw = (w[i >> 2] >> (8 * (i & 3))) & 0xFFu;
-            const uint32_t b = frame0 + 16 * tid + i < nframes ? clamp_width(raw) : 0u;
-            w[i >> 2] = (w[i >> 2] & ~(0xFFu << (8 * (i & 3)))) | (b << (8 * (i & 3)));
-        }
-        s_w4[tid] = w;
-    }
     const u32x4 *src = reinterpret_cast<const u32x4 *>(values) + base;
     if (16ull * (base + agg) <= vsize) {
-        for (uint32_t c = tid; c < agg; c += kThreads)
-            s_in[c] = __builtin_nontemporal_load(src + c);
-    } else {
-        for (uint32_t c = tid; c < agg; c += kThreads)
-            s_in[c] = load16_tail(values, 16ull * (base + c), vsize);
-    }
-    if (tid < 2)
-        s_in[agg + tid] = u32x4{0u, 0u, 0u, 0u};
-    __syncthreads();
-    block_excl_scan<TF>(s_w, s_pref, s_wave);
-    __syncthreads();
-
-    // ---- unpack 2b bytes -> 16 values per lane, store coalesced -----------
-    const uint32_t *s32 = reinterpret_cast<const uint32_t *>(s_in);
-    const bool full = tile_off + TB <= n;
 #pragma unroll
-    for (int k = 0; k < ITEMS; ++k) {
-        const int c = k * kThreads + tid;
-        const int ft = c >> 3;
-        const uint32_t b = s_w[ft];
-        if (b == 0)
-            continue;
-        const uint32_t off = 16u * s_pref[ft] + 2u * b * (uint32_t)(tid & 7);
-        const uint32_t a = off >> 2;
-        const uint64_t w01 = ((uint64_t)s32[a + 1] << 32) | s32[a];
-        const uint64_t w23 = ((uint64_t)s32[a + 3] << 32) | s32[a + 2];
-        uint64_t lo = w01, hi = w23;
-        if (off & 2) {  // 2-byte aligned start: funnel by 16 bits
-            const uint64_t w4 = s32[a + 4];
-            lo = (w01 >> 16) | (w23 << 48);
-            hi = (w23 >> 16) | (w4 << 48);
+        for (int k = 0; k < ITEMS; ++k)
+            if ((uint32_t)(k * kDecThreads + tid) < agg)
+                a[k] = __builtin_nontemporal_load(src + k * kDecThreads + tid);
+    } else {
+#pragma unroll
+        for (int k = 0; k < ITEMS; ++k)
+            if ((uint32_t)(k * kDecThreads + tid) < agg)
+                a[k] = load16_tail(values, 16ull * (base + k * kDecThreads + tid), vsize);
+    }
+}
+
+// The ITEMS (= 8) widths of lane group tid/8, bytes past nframes read as 0.
+__device__ __forceinline__ uint64_t dec_load_widths(const uint8_t *bits, uint64_t f0, uint64_t nframes)
+{
+    if (f0 + 8 <= nframes)
+        return *reinterpret_cast<const uint64_t *>(bits + f0);
+    uint64_t v = 0;
+    uint8_t *p = reinterpret_cast<uint8_t *>(&v);
+    for (int i = 0; i < 8; ++i)
+        p[i] = f0 + i < nframes ? bits[f0 + i] : 0;
+    return v;
+}
+
+template <int ITEMS>
+__global__ __launch_bounds__(kDecThreads, kDecPerCU) void fl_decode_kernel(
+    const uint8_t *__restrict__ bits, uint64_t nframes, const uint8_t *__restrict__ values,
+    uint64_t vsize, uint8_t *__restrict__ out, uint64_t n, const uint64_t *__restrict__ tile_base,
+    uint32_t ntiles, Ctrl *ctrl, uint32_t ticket0)
+{
+    static_assert(ITEMS == 8, "a lane group's widths are one u64");
+    constexpr int T = kDecThreads;
+    constexpr int TB = T * 16 * ITEMS;
+    constexpr int TF = TB / kFrame;
+    __shared__ u32x4 s_in[TB / 16 + 2];  // +2: a lane may read up to 18 bytes past its frame
+    __shared__ uint32_t s_wave[T / kWave];
+    __shared__ uint32_t s_next[2];  // alternating: a slot is rewritten two barriers after its read
+    const int tid = threadIdx.x;
+    const int lane = tid & (kWave - 1);
+    const int wave = tid / kWave;
+    // tiles by ticket (fl_offsets_kernel's workgroups took tickets 0..ticket0-1
+    // of the same counter): workgroups progress through the output in order
+    if (tid == 0)
+        s_next[0] = atomicAdd(&ctrl->ticket, 1u) - ticket0;
+    __syncthreads();
+    uint32_t tile = s_next[0];
+    uint32_t slot = 1;
+    if (tile >= ntiles)
+        return;
+    uint64_t base = tile_base[tile];
+    uint32_t agg = (uint32_t)(tile_base[tile + 1] - base);
+    u32x4 a[ITEMS];
+    dec_load_values<ITEMS>(a, values, base, agg, vsize);
+    uint64_t wv = dec_load_widths(bits, (uint64_t)tile * TF + (tid >> 3) * ITEMS, nframes);
+    for (;;) {
+        if (tid == 0)  // read after the scan barrier below
+            s_next[slot] = atomicAdd(&ctrl->ticket, 1u) - ticket0;
+#pragma unroll
+        for (int k = 0; k < ITEMS; ++k)
+            if ((uint32_t)(k * T + tid) < agg)
+                s_in[k * T + tid] = a[k];
+        if (tid < 2)
+            s_in[agg + tid] = u32x4{0u, 0u, 0u, 0u};
+        // widths (clamped as fl_offsets_kernel clamps them; 0 past the last frame)
+        uint32_t bw[ITEMS];
+        uint32_t gtot = 0;
+#pragma unroll
+        for (int k = 0; k < ITEMS; ++k) {
+            const uint64_t f = (uint64_t)tile * TF + (tid >> 3) * ITEMS + k;
+            const uint32_t b = f < nframes ? clamp_width((uint32_t)(wv >> (8 * k)) & 0xFFu) : 0u;
+            bw[k] = b;
+            gtot += b;
         }
-        const uint64_t p0 = lo;
-        const uint64_t p1 = b == 8 ? hi : ((lo >> (8 * b)) | (hi << (64 - 8 * b)));
-        const uint64_t x0 = unpack8(p0, b);
-        const uint64_t x1 = unpack8(p1, b);
-        const u32x4 r = u32x4{(uint32_t)x0, (uint32_t)(x0 >> 32), (uint32_t)x1,
-                              (uint32_t)(x1 >> 32)};
-        if (full)
-            __builtin_nontemporal_store(r, reinterpret_cast<u32x4 *>(out + tile_off) + c);
-        else
-            store16_tail(out, tile_off + (uint64_t)c * 16, n, r);
+        const uint32_t gincl = wave_incl_scan_u32((lane & 7) == 0 ? gtot : 0u);
+        if (lane == kWave - 1)
+            s_wave[wave] = gincl;
+        __syncthreads();
+        uint32_t wbase = 0;
+#pragma unroll
+        for (int v = 0; v < T / kWave; ++v)
+            wbase += v < wave ? s_wave[v] : 0u;
+
+        // ---- next tile's loads, in flight while this tile is unpacked
+        const uint32_t nxt = s_next[slot];
+        slot ^= 1u;
+        const bool more = nxt < ntiles;
+        const uint64_t tile_off = (uint64_t)tile * TB;
+        if (more) {
+            base = tile_base[nxt];
+            agg = (uint32_t)(tile_base[nxt + 1] - base);
+            dec_load_values<ITEMS>(a, values, base, agg, vsize);
+            wv = dec_load_widths(bits, (uint64_t)nxt * TF + (tid >> 3) * ITEMS, nframes);
+        }
+
+        // ---- unpack 2b bytes -> 16 values per lane and item, store
+        const uint32_t *s32 = reinterpret_cast<const uint32_t *>(s_in);
+        const bool full = tile_off + TB <= n;
+        uint32_t run = wbase + gincl - gtot;  // widths before this group's first frame
+        uint8_t *dst = out + tile_off + (uint32_t)(tid >> 3) * ITEMS * kFrame + (tid & 7) * 16;
+#pragma unroll
+        for (int k = 0; k < ITEMS; ++k) {
+            const uint32_t b = bw[k];
+            const uint32_t off = 16u * run + 2u * b * (uint32_t)(tid & 7);
+            run += b;
+            if (b == 0)
+                continue;
+            const uint32_t ad = off >> 2;
+            const uint64_t w01 = ((uint64_t)s32[ad + 1] << 32) | s32[ad];
+            const uint64_t w23 = ((uint64_t)s32[ad + 3] << 32) | s32[ad + 2];
+            uint64_t lo = w01, hi = w23;
+            if (off & 2) {  // 2-byte aligned start: funnel by 16 bits
+                const uint64_t w4 = s32[ad + 4];
+                lo = (w01 >> 16) | (w23 << 48);
+                hi = (w23 >> 16) | (w4 << 48);
+            }
+            const uint64_t p1 = b == 8 ? hi : ((lo >> (8 * b)) | (hi << (64 - 8 * b)));
+            const uint64_t x0 = unpack8(lo, b);
+            const uint64_t x1 = unpack8(p1, b);
+            const u32x4 r = u32x4{(uint32_t)x0, (uint32_t)(x0 >> 32), (uint32_t)x1,
+                                  (uint32_t)(x1 >> 32)};
+            if (full)
+                __builtin_nontemporal_store(r, reinterpret_cast<u32x4 *>(dst + k * kFrame));
+            else
+                store16_tail(out, (uint64_t)(dst - out) + k * kFrame, n, r);
+        }
+        if (!more)
+            break;
+        tile = nxt;
+        __syncthreads();  // every wave is done reading s_in / s_wave / s_next
     }
 }
 
@@ -576,9 +651,11 @@ extern "C" int flrl_fl_decode_device(const uint8_t *d_bits, size_t bits_size,
                        d_bits, (uint64_t)bits_size, (uint64_t)values_size, (uint64_t)n, tile_base,
                        (uint32_t)L.dec_tiles, (uint32_t)L.off_blocks, (uint32_t)L.off_iters, ctrl, status);
     FLRL_HIP(hipGetLastError());
-    hipLaunchKernelGGL(fl_decode_kernel<kDecItems>, dim3((uint32_t)L.dec_tiles), dim3(kThreads), 0,
+    const size_t dgrid = (size_t)kDecPerCU * (size_t)cu_count();
+    hipLaunchKernelGGL(fl_decode_kernel<kDecItems>,
+                       dim3((uint32_t)(L.dec_tiles < dgrid ? L.dec_tiles : dgrid)), dim3(kDecThreads), 0,
                        s, d_bits, (uint64_t)bits_size, d_values, (uint64_t)values_size, d_out,
-                       (uint64_t)n, tile_base);
+                       (uint64_t)n, tile_base, (uint32_t)L.dec_tiles, ctrl, (uint32_t)L.off_blocks);
     FLRL_HIP(hipGetLastError());
     return FLRL_OK;
 }

@@ -90,7 +90,8 @@ def test_generated_golden(golden, idx):
 
 
 SIZES = [1, 2, 7, 8, 15, 16, 17, 127, 128, 129, 255, 256, 1000, 4096, 4741, 65535, 65536,
-         65537, 100003, 131072, 131073, 262144 + 4095, (1 << 20) + 13]
+         65537, 100003, 131071, 131072, 131073, 196607, 196609, 262144 + 4095, 327744,
+         (1 << 20) + 13]  # decode tiles are 64 KiB, encode tiles 128 KiB
 
 
 @pytest.mark.parametrize("n", SIZES)
