@@ -327,18 +327,30 @@ __global__ __launch_bounds__(kThreads) void fl_offsets_kernel(
     bool has_last = false;       // this lane holds the last frame
     uint64_t last_local = 0;     // its units before the last frame, workgroup-relative
     bool bad = false;
+    uint64_t keep = 0;
     for (uint32_t it = 0; it < iters; ++it) {
         const uint64_t f0 = ((uint64_t)blk * iters + it) * kOffFrames + (uint64_t)tid * kOffFramesPerThread;
+        // all of the lane's width loads in flight before any is used
+        constexpr int Q = kOffFramesPerThread / 16;
+        u32x4 wq[Q];
+        if (f0 + kOffFramesPerThread <= nframes) {
+#pragma unroll
+            for (int q = 0; q < Q; ++q)
+                wq[q] = *reinterpret_cast<const u32x4 *>(bits + f0 + 16 * q);
+        } else {
+#pragma unroll
+            for (int q = 0; q < Q; ++q)
+                wq[q] = load16_tail(bits, f0 + 16 * q, nframes);
+        }
         // widths 4 per dword (SWAR): a byte is invalid if it is 0 or > 8
         uint32_t sum = 0;
 #pragma unroll
-        for (int q = 0; q < kOffFramesPerThread / 16; ++q) {
+        for (int q = 0; q < Q; ++q) {
             const uint64_t fq = f0 + 16 * q;
             if (fq + 16 <= nframes) {
-                const u32x4 w = *reinterpret_cast<const u32x4 *>(bits + fq);
 #pragma unroll
                 for (int d = 0; d < 4; ++d) {
-                    const uint32_t x = w[d];
+                    const uint32_t x = wq[q][d];
                     const uint32_t zero = (x - 0x01010101u) & ~x & 0x80808080u;
                     const uint32_t big = (((x & 0x7F7F7F7Fu) + 0x77777777u) | x) & 0x80808080u;
                     if (zero | big) {  // rare: clamp byte by byte
@@ -352,7 +364,7 @@ __global__ __launch_bounds__(kThreads) void fl_offsets_kernel(
                 }
             } else {
                 for (int i = 0; i < 16 && fq + i < nframes; ++i) {
-                    const uint32_t raw = bits[fq + i];
+                    const uint32_t raw = (wq[q][i >> 2] >> (8 * (i & 3))) & 0xFFu;
                     bad |= raw < 1 || raw > 8;
                     sum += clamp_width(raw);
                 }
@@ -373,8 +385,12 @@ __global__ __launch_bounds__(kThreads) void fl_offsets_kernel(
         }
         const uint32_t excl = before + inc - sum;
         const uint64_t tile = f0 / kDecTileFrames;
-        if (tid % kOffLanesPerTile == 0 && tile < ntiles)
-            tile_base[tile] = local + excl;
+        if (tid % kOffLanesPerTile == 0 && tile < ntiles) {
+            if (iters == 1)
+                keep = local + excl;  // one round: the entry waits in a register for the base
+            else
+                tile_base[tile] = local + excl;
+        }
         if (nframes > f0 && nframes <= f0 + kOffFramesPerThread) {
             has_last = true;
             last_local = local + excl + sum - clamp_width(bits[nframes - 1]);
@@ -388,7 +404,7 @@ __global__ __launch_bounds__(kThreads) void fl_offsets_kernel(
         const uint64_t f0 = ((uint64_t)blk * iters + it) * kOffFrames + (uint64_t)tid * kOffFramesPerThread;
         const uint64_t tile = f0 / kDecTileFrames;
         if (tid % kOffLanesPerTile == 0 && tile < ntiles)
-            tile_base[tile] += base;  // this lane's own entry
+            tile_base[tile] = iters == 1 ? keep + base : tile_base[tile] + base;  // this lane's own entry
     }
     if (blk + 1 == nblocks && tid == 0)
         tile_base[ntiles] = base + local;
@@ -401,15 +417,18 @@ __global__ __launch_bounds__(kThreads) void fl_offsets_kernel(
     }
 }
 
-// Decode: persistent grid-stride workgroups (kDecPerCU per CU) over 32 KiB
-// output tiles; the packed bytes (and frame widths) of a workgroup's next tile
-// are loaded into registers right after the current tile's width scan, while
-// the current tile is unpacked from LDS. Lane group g = tid/8 owns frames
-// g*ITEMS .. +ITEMS-1 of the tile (its prefix is a register running sum after
-// one wave scan); lane tid%8 unpacks 16-byte chunk tid%8 of each. Measured
-// against the one-tile-per-workgroup form (scripts/ubench_decode.hip): -5 %
-// on 1 GiB u8 and lo4; contiguous per-workgroup tile ranges (which would let
-// the offsets pre-pass fuse into this kernel) were 20 % slower.
+// Decode: persistent 512-thread workgroups (kDecPerCU per CU) take 64 KiB
+// output tiles by ticket; the packed bytes (and frame widths) of a workgroup's
+// next tile are loaded into registers right after the current tile's width
+// scan, while the current tile is unpacked from LDS. Lane group g = tid/8 owns
+// frames g*ITEMS .. +ITEMS-1 of the tile (its prefix is a register running sum
+// after one wave scan); lane tid%8 unpacks 16-byte chunk tid%8 of each.
+// Measured against one 32 KiB tile per workgroup (scripts/ubench_decode.hip):
+// -6 % at 1 GiB u8, -5 % lo4, -13 % at 16 GiB. Grid-stride tiles instead of
+// tickets were as good at 1 GiB but 10 % slower at 16 GiB (workgroups drift
+// apart in the address space); 32 KiB tiles by ticket saturate the ticket
+// atomic; contiguous per-workgroup tile ranges (which would let the offsets
+// pre-pass fuse into this kernel) were 20 % slower.
 template <int ITEMS>
 __device__ __forceinline__ void dec_load_values(u32x4 (&a)[ITEMS], const uint8_t *values, uint64_t base,
                                                 uint32_t agg, uint64_t vsize)

@@ -738,13 +738,26 @@ __global__ __launch_bounds__(kThreads) void rl_offsets_kernel(
     constexpr int kLanesPerTile = kRdRuns / kRoRunsPerThread;
     uint64_t local = 0;  // output bytes before this round, workgroup-relative
     bool bad = false;
+    uint64_t keep = 0;
     for (uint32_t it = 0; it < iters; ++it) {
         const uint64_t r0 = ((uint64_t)blk * iters + it) * kRoRuns + (uint64_t)tid * kRoRunsPerThread;
+        // all of the lane's count loads in flight before any is used
+        constexpr int Q = kRoRunsPerThread / 16;
+        u32x4 cq[Q];
+        if (r0 + kRoRunsPerThread <= runs) {
+#pragma unroll
+            for (int q = 0; q < Q; ++q)
+                cq[q] = *reinterpret_cast<const u32x4 *>(counts + r0 + 16 * q);
+        } else {
+#pragma unroll
+            for (int q = 0; q < Q; ++q)
+                cq[q] = load16_tail(counts, r0 + 16 * q, runs);
+        }
         uint32_t sum = 0;
-#pragma unroll 4
-        for (int q = 0; q < kRoRunsPerThread / 16; ++q) {
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
             const uint64_t rq = r0 + 16 * q;
-            const u32x4 v = load16_tail(counts, rq, runs);
+            const u32x4 v = cq[q];
 #pragma unroll
             for (int d = 0; d < 4; ++d) {
                 const uint32_t x = v[d];
@@ -771,8 +784,12 @@ __global__ __launch_bounds__(kThreads) void rl_offsets_kernel(
             agg += s_wave[v];
         }
         const uint64_t tile = r0 / kRdRuns;
-        if (tid % kLanesPerTile == 0 && tile < ntiles)
-            tile_base[tile] = local + before + inc - sum;
+        if (tid % kLanesPerTile == 0 && tile < ntiles) {
+            if (iters == 1)
+                keep = local + before + inc - sum;  // one round: the entry waits in a register for the base
+            else
+                tile_base[tile] = local + before + inc - sum;
+        }
         local += agg;
     }
     if (bad)
@@ -783,7 +800,7 @@ __global__ __launch_bounds__(kThreads) void rl_offsets_kernel(
         const uint64_t r0 = ((uint64_t)blk * iters + it) * kRoRuns + (uint64_t)tid * kRoRunsPerThread;
         const uint64_t tile = r0 / kRdRuns;
         if (tid % kLanesPerTile == 0 && tile < ntiles)
-            tile_base[tile] += base;  // this lane's own entry
+            tile_base[tile] = iters == 1 ? keep + base : tile_base[tile] + base;  // this lane's own entry
     }
     if (blk + 1 == nblocks && tid == 0) {
         tile_base[ntiles] = base + local;
