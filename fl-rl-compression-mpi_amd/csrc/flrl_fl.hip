@@ -10,15 +10,16 @@
 // widths — no bit cursor, no atomics on the data path.
 //
 // Encode (fl_encode_kernel) reads the input once (N+F+V bytes of HBM traffic).
-// It is a persistent, software-pipelined kernel with one 512-thread workgroup
-// per CU taking 128 KiB tiles by ticket: for the tile it holds in registers it
-// computes frame widths (OR of the frame's bytes), scans them in LDS, publishes
-// the tile's width sum and packs into an LDS staging tile; then it issues the
-// loads of its NEXT tile, resolves the current tile's global offset by
-// decoupled look-back (wave 0) and streams the packed tile out in coalesced
-// 16-byte stores (offsets are multiples of 16). HBM loads of tile t+1 are in
-// flight across tile t's look-back and stores. Tile size, workgroup shape and
-// the look-back ordering were chosen by measurement (scripts/ubench_encode.hip,
+// It is a persistent, software-pipelined kernel with one workgroup per CU
+// (8 data waves + 1 look-back wave) taking 128 KiB tiles by ticket: for the
+// tile the data waves hold in registers they compute frame widths (OR of the
+// frame's bytes) and scan them; the look-back wave publishes the tile's width
+// sum and resolves its global offset by decoupled look-back WHILE the data
+// waves pack into an LDS staging tile and issue the loads of their NEXT tile;
+// then the packed tile streams out in coalesced 16-byte stores (offsets are
+// multiples of 16). HBM loads of tile t+1 are in flight across tile t's
+// look-back and stores. Tile size, workgroup shape and the look-back ordering
+// were chosen by measurement (scripts/ubench_encode.hip, scripts/ab_encode.py,
 // DESIGN.md §Encode).
 //
 // Decode is two launches: fl_offsets_kernel scans the frame widths (F bytes,
@@ -47,7 +48,7 @@
 
 namespace flrl {
 
-constexpr int kEncThreads = 512;  // encode workgroup: 8 waves, one per CU (LDS 133 KB)
+constexpr int kEncThreads = 512;  // encode data threads: 8 waves + 1 look-back wave, one workgroup per CU (LDS 133 KB)
 constexpr int kEncItems = 16;     // encode tile = 512 lanes x 16 x 16 B = 128 KiB (1024 frames)
 constexpr int kEncTileBytes = kEncThreads * 16 * kEncItems;
 constexpr int kDecThreads = 512;  // decode workgroup: 8 waves
@@ -133,24 +134,25 @@ __device__ __forceinline__ void stage_packed(uint8_t *s, uint32_t off, uint32_t 
     }
 }
 
-// FL encode: persistent, one T-thread workgroup per CU, 16*T*ITEMS-byte tiles
-// (128 KiB at T = 512, ITEMS = 16) taken by ticket. Per tile: widths (OR of
-// each frame's 8 lanes); a lane group's 16 frames are consecutive, so frame
+// FL encode: persistent, one (T + 64)-thread workgroup per CU, 16*T*ITEMS-byte
+// tiles (128 KiB at T = 512, ITEMS = 16) taken by ticket. Per tile: widths (OR
+// of each frame's 8 lanes); a lane group's 16 frames are consecutive, so frame
 // offsets are a register running sum after one wave scan of group totals and
-// one LDS exchange of wave totals (2 barriers per tile in all); publish the
-// width sum, pack into the LDS staging tile, prefetch the next tile into the
-// freed registers, resolve the tile's offset by look-back (wave 0), stream the
-// staged bytes out. Wave 0
-// issues its share of the prefetch only after its look-back: vmcnt is per wave
-// and in order, so status loads issued behind 16 bulk loads would each wait
-// for all of them (measured: scripts/ubench_encode.hip).
+// one LDS exchange of wave totals (2 barriers per tile in all). The extra wave
+// publishes the width sum and resolves the tile's offset by look-back while
+// the T data threads pack into the LDS staging tile and prefetch the next tile
+// into the freed registers; then the staged bytes stream out. The look-back
+// wave issues no bulk memory operations: vmcnt is per wave and in order, so
+// its status loads would otherwise wait behind them. A/B against the look-back
+// done by data wave 0 (scripts/ab_encode.py): lo4 -11 %, zero -3 %, 16 GiB u8
+// -2 %, 1 GiB u8 equal.
 // Per-tile timestamp hook for scripts/ubench_fl.hip (no-op in the library).
 #ifndef FLRL_FL_TRACE
 #define FLRL_FL_TRACE(tile, k) ((void)0)
 #endif
 
 template <int T, int ITEMS>
-__global__ __launch_bounds__(T, 1) void fl_encode_kernel(
+__global__ __launch_bounds__(T + kWave, 1) void fl_encode_kernel(
     const uint8_t *__restrict__ in, uint64_t n, uint64_t nframes, uint32_t ntiles,
     uint8_t *__restrict__ bits, uint8_t *__restrict__ values, uint64_t *__restrict__ values_size,
     Ctrl *ctrl, uint64_t *status)
@@ -168,6 +170,9 @@ __global__ __launch_bounds__(T, 1) void fl_encode_kernel(
 
     const int tid = threadIdx.x;
     const int wave = tid / kWave;
+    // wave T/64 (the look-back wave) holds no tile data: it publishes and
+    // resolves the look-back while the T data threads pack and prefetch
+    const bool lw = tid >= T;
     if (tid == 0)
         s_next = atomicAdd(&ctrl->ticket, 1u);
     __syncthreads();
@@ -175,7 +180,8 @@ __global__ __launch_bounds__(T, 1) void fl_encode_kernel(
     if (tile >= ntiles)
         return;
     u32x4 a[ITEMS];
-    load_tile_g<T, ITEMS>(a, in, (uint64_t)tile * TB, n);
+    if (!lw)
+        load_tile_g<T, ITEMS>(a, in, (uint64_t)tile * TB, n);
 
     for (;;) {
         // no barrier here: s_out/s_w of the previous tile are re-written only
@@ -190,28 +196,30 @@ __global__ __launch_bounds__(T, 1) void fl_encode_kernel(
         // and the scan: a lane group's frames are consecutive, so its prefix is a
         // register running sum; groups scan across the wave, waves through LDS
         uint32_t bw[ITEMS];
-        uint32_t gtot = 0;
-        u32x4 wv = u32x4{0u, 0u, 0u, 0u};
+        uint32_t gtot = 0, gincl = 0;
+        if (!lw) {
+            u32x4 wv = u32x4{0u, 0u, 0u, 0u};
 #pragma unroll
-        for (int k = 0; k < ITEMS; ++k) {
-            uint32_t o = a[k].x | a[k].y | a[k].z | a[k].w;
-            o |= o >> 16;
-            o |= o >> 8;
-            o = or_8lanes(o & 0xFFu);
-            uint32_t b = o ? 32u - __clz(o) : 1u;
-            const int ft = (tid >> 3) * ITEMS + k;
-            if (frame0 + ft >= nframes)
-                b = 0;  // past the last frame: contributes nothing
-            bw[k] = b;
-            gtot += b;
-            wv[k >> 2] |= b << (8 * (k & 3));
+            for (int k = 0; k < ITEMS; ++k) {
+                uint32_t o = a[k].x | a[k].y | a[k].z | a[k].w;
+                o |= o >> 16;
+                o |= o >> 8;
+                o = or_8lanes(o & 0xFFu);
+                uint32_t b = o ? 32u - __clz(o) : 1u;
+                const int ft = (tid >> 3) * ITEMS + k;
+                if (frame0 + ft >= nframes)
+                    b = 0;  // past the last frame: contributes nothing
+                bw[k] = b;
+                gtot += b;
+                wv[k >> 2] |= b << (8 * (k & 3));
+            }
+            const int lane = tid & (kWave - 1);
+            gincl = wave_incl_scan_u32((lane & 7) == 0 ? gtot : 0u);
+            if (lane == kWave - 1)
+                s_wave[wave] = gincl;
+            if ((tid & 7) == 0)
+                s_w4[tid >> 3] = wv;
         }
-        const int lane = tid & (kWave - 1);
-        const uint32_t gincl = wave_incl_scan_u32((lane & 7) == 0 ? gtot : 0u);
-        if (lane == kWave - 1)
-            s_wave[wave] = gincl;
-        if ((tid & 7) == 0)
-            s_w4[tid >> 3] = wv;
         __syncthreads();
         const uint32_t nxt = s_next;
         uint32_t wbase = 0, agg = 0;
@@ -221,79 +229,89 @@ __global__ __launch_bounds__(T, 1) void fl_encode_kernel(
             wbase += v < wave ? t : 0u;
             agg += t;
         }
-
-        // ---- publish the tile's width sum early (successors' look-backs need it)
-        if (tid == 0)
-            publish_aggregate(status, tile, agg);
-        FLRL_FL_TRACE(tile, 1);
-
-        // ---- bits[] for this tile's frames
-        // (not by wave 0: its look-back status loads would queue behind these
-        // stores, vmcnt being in order)
-        if (frame0 + TF <= nframes) {
-            for (int i = tid - kWave; i >= 0 && i < TF / 16; i += T - kWave)
-                reinterpret_cast<u32x4 *>(bits + frame0)[i] = s_w4[i];
-        } else {
-            for (int i = tid - kWave; i >= 0 && i < TF; i += T - kWave)
-                if (frame0 + i < nframes)
-                    bits[frame0 + i] = s_w[i];
-        }
-
-        // ---- pack 16 values -> 2b bytes per lane into the LDS staging tile
-        uint32_t run = wbase + gincl - gtot;  // widths before this group's first frame
-#pragma unroll
-        for (int k = 0; k < ITEMS; ++k) {
-            const uint32_t b = bw[k];
-            const uint32_t off = 16u * run + 2u * b * (uint32_t)(tid & 7);
-            run += b;
-            if (b == 0)
-                continue;
-            const uint64_t x0 = ((uint64_t)a[k].y << 32) | a[k].x;
-            const uint64_t x1 = ((uint64_t)a[k].w << 32) | a[k].z;
-            uint64_t lo = x0, hi = x1;
-            if (b != 8) {
-                const uint64_t p0 = pack8(x0, b), p1 = pack8(x1, b);
-                lo = p0 | (p1 << (8 * b));
-                hi = p1 >> (64 - 8 * b);
-            }
-            stage_packed(s_out_b, off, b, lo, hi);
-        }
-
-        // ---- prefetch the next tile into the freed registers (wave 0: later)
         const bool more = nxt < ntiles;
-        if (more && wave != 0)
-            load_tile_g<T, ITEMS>(a, in, (uint64_t)nxt * TB, n);
-        if (wave == 0) {
+
+        if (lw) {
+            // ---- the look-back wave: publish, resolve (concurrent with the pack;
+            // it issues no bulk loads or stores, so its status loads never wait
+            // behind them -- vmcnt is per wave and in order)
+            if (tid == T)
+                publish_aggregate(status, tile, agg);
+            FLRL_FL_TRACE(tile, 1);
             const uint64_t excl = lookback_resolve(status, tile, agg, ctrl);
-            if (tid == 0)
+            if (tid == T)
                 s_base = excl;
             FLRL_FL_TRACE(tile, 2);
-            if (more)
-                load_tile_g<T, ITEMS>(a, in, (uint64_t)nxt * TB, n);
+        } else {
+            // ---- bits[] for this tile's frames
+            if (frame0 + TF <= nframes) {
+                for (int i = tid; i < TF / 16; i += T)
+                    reinterpret_cast<u32x4 *>(bits + frame0)[i] = s_w4[i];
+            } else {
+                for (int i = tid; i < TF; i += T)
+                    if (frame0 + i < nframes)
+                        bits[frame0 + i] = s_w[i];
+            }
         }
+
+        if (!lw) {
+            // ---- pack 16 values -> 2b bytes per lane into the LDS staging tile
+            uint32_t run = wbase + gincl - gtot;  // widths before this group's first frame
+#pragma unroll
+            for (int k = 0; k < ITEMS; ++k) {
+                const uint32_t b = bw[k];
+                const uint32_t off = 16u * run + 2u * b * (uint32_t)(tid & 7);
+                run += b;
+                if (b == 0)
+                    continue;
+                const uint64_t x0 = ((uint64_t)a[k].y << 32) | a[k].x;
+                const uint64_t x1 = ((uint64_t)a[k].w << 32) | a[k].z;
+                uint64_t lo = x0, hi = x1;
+                if (b != 8) {
+                    const uint64_t p0 = pack8(x0, b), p1 = pack8(x1, b);
+                    lo = p0 | (p1 << (8 * b));
+                    hi = p1 >> (64 - 8 * b);
+                }
+                stage_packed(s_out_b, off, b, lo, hi);
+            }
+        }
+
+        // ---- prefetch the next tile into the freed registers
+        if (more && !lw)
+            load_tile_g<T, ITEMS>(a, in, (uint64_t)nxt * TB, n);
         __syncthreads();
 
         // ---- stream the packed tile out: 16-B aligned, coalesced
         const uint64_t base = s_base;  // in 16-byte units
         u32x4 *dst = reinterpret_cast<u32x4 *>(values) + base;
-        if (tile + 1 < ntiles) {
-            u32x4 o[ITEMS];  // static trip count: LDS reads hoisted, stores predicated
+        if (!lw) {
+            if (tile + 1 < ntiles) {
+                // static trip count: LDS reads hoisted, stores predicated; in two
+                // halves, as the registers also hold the prefetched tile
+                constexpr int SPLIT = 2;
 #pragma unroll
-            for (int k = 0; k < ITEMS; ++k)
-                o[k] = s_out[k * T + tid];
+                for (int h = 0; h < SPLIT; ++h) {
+                    u32x4 o[ITEMS / SPLIT];
 #pragma unroll
-            for (int k = 0; k < ITEMS; ++k)
-                if ((uint32_t)(k * T + tid) < agg)
-                    __builtin_nontemporal_store(o[k], dst + k * T + tid);
-        } else {
-            // last tile: valuesSize = 16*(frames before last) + ceil(cnt*b_last/8)
-            const int fl = (int)(nframes - 1 - frame0);
-            const uint64_t cnt = n - (nframes - 1) * kFrame;
-            const uint64_t vsize = 16ull * (base + agg - s_w[fl]) + (cnt * s_w[fl] + 7) / 8;
-            if (tid == 0)
-                *values_size = vsize;
-            for (uint32_t c = tid; c < agg; c += T)
-                store16_tail(values, 16ull * (base + c), vsize, s_out[c]);
+                    for (int k = 0; k < ITEMS / SPLIT; ++k)
+                        o[k] = s_out[(h * ITEMS / SPLIT + k) * T + tid];
+#pragma unroll
+                    for (int k = 0; k < ITEMS / SPLIT; ++k) {
+                        const uint32_t c = (h * ITEMS / SPLIT + k) * T + tid;
+                        if (c < agg)
+                            __builtin_nontemporal_store(o[k], dst + c);
+                    }
+                }
+            } else {
+                // last tile: valuesSize = 16*(frames before last) + ceil(cnt*b_last/8)
+                const int fl = (int)(nframes - 1 - frame0);
+                const uint64_t cnt = n - (nframes - 1) * kFrame;
+                const uint64_t vsize = 16ull * (base + agg - s_w[fl]) + (cnt * s_w[fl] + 7) / 8;
+                if (tid == 0)
+                    *values_size = vsize;
+                for (uint32_t c = tid; c < agg; c += T)
+                    store16_tail(values, 16ull * (base + c), vsize, s_out[c]);
+            }
         }
         FLRL_FL_TRACE(tile, 3);
         if (!more)
@@ -628,10 +646,9 @@ extern "C" int flrl_fl_encode_device(const uint8_t *d_in, size_t n, uint8_t *d_b
     uint64_t *status = reinterpret_cast<uint64_t *>(ctrl + 1);
     const size_t resident = (size_t)cu_count();
     const uint32_t grid = (uint32_t)(L.enc_tiles < resident ? L.enc_tiles : resident);
-    hipLaunchKernelGGL((fl_encode_kernel<kEncThreads, kEncItems>), dim3(grid), dim3(kEncThreads), 0,
-                       s, d_in,
-                       (uint64_t)n, (uint64_t)div_up(n, kFrame), (uint32_t)L.enc_tiles, d_bits,
-                       d_values, d_values_size, ctrl, status);
+    hipLaunchKernelGGL((fl_encode_kernel<kEncThreads, kEncItems>), dim3(grid), dim3(kEncThreads + kWave),
+                       0, s, d_in, (uint64_t)n, (uint64_t)div_up(n, kFrame), (uint32_t)L.enc_tiles,
+                       d_bits, d_values, d_values_size, ctrl, status);
     FLRL_HIP(hipGetLastError());
     return FLRL_OK;
 }
