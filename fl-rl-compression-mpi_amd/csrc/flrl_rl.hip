@@ -24,12 +24,15 @@
 // first natural head are written and the staged runs leave contiguously.
 //
 // Decode: rl_offsets_kernel scans the counts (R bytes) into per-tile output
-// offsets (and validates them); rl_decode_kernel (3 workgroups per CU,
+// offsets (and validates them); rl_decode_kernel (4 workgroups per CU,
 // grid-stride, the next tile's counts and values prefetched into registers)
-// then expands each tile of 4096 runs independently, in 32 KiB LDS output
-// windows: the runs overlapping a window memset their bytes into it with
-// aligned dword stores, and the window leaves in 16-byte stores (the two chunks
-// a tile shares with its neighbours byte by byte).
+// then expands each tile of 4096 runs independently. Output-driven: per 64 KiB
+// window the runs starting in it set bits in an LDS bitmap, a popcount scan
+// ranks every 16-byte chunk, and each lane assembles whole chunks (byte
+// permutes over the 16 values from the chunk's first run on) and stores them
+// coalesced from registers. Dense tiles (<= 32 KiB of output) memset their runs
+// into an LDS byte window instead. Chunks a tile shares with its neighbours are
+// written byte by byte.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdlib.h>
@@ -65,8 +68,7 @@ constexpr int kRlStageBytes = 16256;  // LDS run staging (48 KiB of LDS per work
 
 constexpr int kRdRuns = 4096;        // runs per decode tile
 constexpr int kRdThreads = 256;
-constexpr int kRdWindow = 32768;     // LDS output window (bytes)
-constexpr int kRdPerCU = 3;          // resident decode workgroups per CU (LDS 53 KB each)
+constexpr int kRdPerCU = 4;          // resident decode workgroups per CU (LDS 37 KB each)
 constexpr int kRoRunsPerThread = 256;
 constexpr int kRoRuns = kRoRunsPerThread * kThreads;  // runs per offsets workgroup
 static_assert(kRdRuns % kRoRunsPerThread == 0, "whole offsets lanes per decode tile");
@@ -809,44 +811,52 @@ __global__ __launch_bounds__(kThreads) void rl_offsets_kernel(
     }
 }
 
-// ---- decode: expand one tile of kRdRuns runs ------------------------------
-// The tile's output [base, end) is produced in kRdWindow-byte windows aligned to
-// global 16-byte boundaries: the runs overlapping a window memset their bytes into an LDS window with
-// aligned dword stores, then the window leaves in 16-byte stores (the two
-// chunks a tile shares with its neighbours byte by byte).
-__device__ __forceinline__ uint32_t run_lower(const uint32_t *pre, uint32_t nr, uint32_t x)
-{
-    // last j in [0, nr) with pre[j] <= x (pre[0] = 0 <= x)
-    uint32_t a = 0, b = nr;
-    while (b - a > 1) {
-        const uint32_t m = (a + b) >> 1;
-        if (pre[m] <= x)
-            a = m;
-        else
-            b = m;
-    }
-    return a;
-}
+// ---- decode by rank: output-driven windows ---------------------------------
+// Every lane produces whole 16-byte output chunks, stored coalesced straight
+// from registers. Per kRkWindow-byte window of a tile's output: (1) each run
+// starting in the window sets its start bit in an LDS bitmap (ds_or), (2) a
+// block scan of the bitmap words' popcounts gives, for every chunk, the number
+// of runs that start before it, so (3) the run covering a chunk's first byte
+// is (runs before the window) + (starts up to that byte) - 1; byte i of the
+// chunk takes run r + k_i (k_i = start bits in bytes 1..i, an in-register byte
+// prefix sum), gathered from the 16 values from run r on by byte permutes. No
+// per-byte LDS stores, no LDS staging of the output. Lanes mark runs strided
+// (lane t: runs t, t+256, ...) so one ds_or instruction targets consecutive
+// runs' words, not words 16 runs apart (a 16-way bank conflict). Tiles with at
+// most kRkDense bytes of output (mean run <= 8) keep the memset path. Output
+// stores are plain (write-back) stores: with non-temporal stores the same
+// kernel takes 0.335 instead of 0.281 ms on 1 GiB runs32 (scripts/ab_rl_decode.py).
+// Measured against the LDS-window memset decode (scripts/ab_rl_decode.py, one
+// process, decode call incl. offsets pre-pass): runs32 0.338 -> 0.290 ms,
+// longruns 0.313 -> 0.272, random bytes 1.74 -> 1.24, lo4 1.79 -> 1.29.
+constexpr int kRkWindow = 65536;            // output bytes per window
+constexpr int kRkWords = kRkWindow / 32;    // bitmap words per window
+constexpr int kRkDense = 32768;             // tiles with at most this much output: per-thread memsets
 
 __global__ __launch_bounds__(kRdThreads) void rl_decode_kernel(
     const uint8_t *__restrict__ counts, const uint8_t *__restrict__ values, uint64_t runs,
     uint8_t *__restrict__ out, uint64_t n, const uint64_t *__restrict__ tile_base, uint64_t ntiles)
 {
-    __shared__ uint32_t s_pre[kRdRuns + 1];  // local output offset of each run
-    __shared__ u32x4 s_val4[kRdRuns / 16];
-    __shared__ u32x4 s_win4[kRdWindow / 16];
-    __shared__ uint32_t s_wave[kRdThreads / kWave];
-    __shared__ uint32_t s_next;
-    uint8_t *s_val = reinterpret_cast<uint8_t *>(s_val4);
-    uint8_t *s_win = reinterpret_cast<uint8_t *>(s_win4);
-    uint32_t *s_win32 = reinterpret_cast<uint32_t *>(s_win4);
+    constexpr int T = kRdThreads;
+    constexpr int RPT = kRdRuns / T;        // runs per thread
+    constexpr int WPT = kRkWords / T;       // bitmap words per thread (scan)
+    constexpr int CPT = kRkWindow / 16 / T; // chunks per thread per window
+    static_assert(RPT == 16 && WPT == 8, "one 16-byte count/value vector, two bitmap vectors per thread");
+    // [bitmap: kRkWords][s_pre: kRkWords][s_st: kRdRuns + 1] u32; a dense tile
+    // (output <= kRkDense bytes) uses the same LDS as its byte output window
+    __shared__ u32x4 s_big4[(2 * kRkWords + kRdRuns + 1 + 3) / 4];
+    __shared__ u32x4 s_val4[kRdRuns / 16 + 1];  // +16 B: the permute window reads up to 19 bytes past a run
+    __shared__ uint32_t s_wave[T / kWave];
+    static_assert(sizeof(s_big4) >= kRkDense, "dense window fits the aliased LDS");
+    u32x4 *const s_bm4 = s_big4;
+    uint32_t *const s_bm = reinterpret_cast<uint32_t *>(s_big4);
+    uint32_t *const s_pre = s_bm + kRkWords;  // runs starting in the window before word w
+    uint32_t *const s_st = s_pre + kRkWords;  // tile-local start of each run (+ the tile's total)
+    const uint8_t *s_val = reinterpret_cast<const uint8_t *>(s_val4);
     const int tid = threadIdx.x;
     const int lane = tid & (kWave - 1);
     const int wave = tid / kWave;
-    constexpr int RPT = kRdRuns / kRdThreads;
-    static_assert(RPT == 16, "one 16-byte count vector and one value vector per thread");
-    // grid-stride over decode tiles; the next tile's counts, values and bounds
-    // are loaded into registers while this one is expanded
+
     uint64_t tile = blockIdx.x;
     if (tile >= ntiles)
         return;
@@ -854,124 +864,205 @@ __global__ __launch_bounds__(kRdThreads) void rl_decode_kernel(
     u32x4 vv = load16_tail(values, tile * kRdRuns + tid * RPT, runs);
     uint64_t base = tile_base[tile], end = tile_base[tile + 1];
     for (;;) {
-    const uint64_t r0 = tile * kRdRuns;
-    const uint64_t next = tile + gridDim.x;
-    __syncthreads();  // the previous tile's LDS readers are done
-    const bool skip = end > n || base >= end;  // empty, or malformed (flagged by rl_offsets_kernel)
-    const uint32_t nr = (uint32_t)(runs - r0 < (uint64_t)kRdRuns ? runs - r0 : kRdRuns);
-    uint32_t c[RPT];
-    uint32_t sum = 0;
-    s_val4[tid] = vv;
-    const u32x4 vv_cur = vv;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-        c[i] = (cv[i >> 2] >> (8 * (i & 3))) & 0xFFu;
-        sum += c[i];
-    }
-    const uint64_t cbase = base, cend = end;
-    if (next < ntiles) {
-        cv = load16_tail(counts, next * kRdRuns + tid * RPT, runs);
-        vv = load16_tail(values, next * kRdRuns + tid * RPT, runs);
-        base = tile_base[next];
-        end = tile_base[next + 1];
-    }
-    if (!skip) {
-    const uint32_t inc = wave_incl_scan_u32(sum);
-    if (lane == kWave - 1)
-        s_wave[wave] = inc;
-    __syncthreads();
-    uint32_t before = 0;
-#pragma unroll
-    for (int v = 0; v < kRdThreads / kWave; ++v)
-        before += v < wave ? s_wave[v] : 0u;
-    const uint32_t run0 = before + inc - sum;  // output offset of this thread's first run
-    uint32_t run = run0;
-#pragma unroll
-    for (int i = 0; i < RPT; ++i) {
-        s_pre[tid * RPT + i] = run;
-        run += c[i];
-    }
-    if (tid == 0)
-        s_pre[kRdRuns] = (uint32_t)(cend - cbase);
-    const uint64_t g0 = cbase & ~15ull;
-    if (cend - g0 <= (uint64_t)kRdWindow) {
-        // the whole tile fits one window (short runs): every thread memsets its
-        // own 16 runs from registers, no LDS look-ups
-        const uint32_t shift = (uint32_t)(cbase - g0);
-        uint32_t p = run0 + shift;
+        const uint64_t next = tile + gridDim.x;
+        __syncthreads();  // the previous tile's LDS readers are done
+        const bool skip = end > n || base >= end;  // empty, or malformed (flagged by rl_offsets_kernel)
+        const uint64_t cbase = base, cend = end;
+        s_val4[tid] = vv;
+        const u32x4 vv_cur = vv;
+        uint32_t c[RPT];
+        uint32_t sum = 0;
 #pragma unroll
         for (int i = 0; i < RPT; ++i) {
-            const uint8_t v = (uint8_t)(vv_cur[i >> 2] >> (8 * (i & 3)));
-            const uint32_t q = p + c[i];
-            for (; p < q; ++p)
-                s_win[p] = v;
+            c[i] = (cv[i >> 2] >> (8 * (i & 3))) & 0xFFu;
+            sum += c[i];
         }
-        __syncthreads();
-        const uint32_t wlen = (uint32_t)(cend - g0);
-        for (uint32_t ch = tid; ch * 16 < wlen; ch += kRdThreads) {
-            const uint64_t gp = g0 + 16ull * ch;
-            if (gp >= cbase && gp + 16 <= cend) {
-                __builtin_nontemporal_store(s_win4[ch], reinterpret_cast<u32x4 *>(out + gp));
+        if (next < ntiles) {  // next tile's loads in flight during this one
+            cv = load16_tail(counts, next * kRdRuns + tid * RPT, runs);
+            vv = load16_tail(values, next * kRdRuns + tid * RPT, runs);
+            base = tile_base[next];
+            end = tile_base[next + 1];
+        }
+        if (!skip) {
+            const uint32_t inc = wave_incl_scan_u32(sum);
+            if (lane == kWave - 1)
+                s_wave[wave] = inc;
+#pragma unroll
+            for (int q = 0; q < WPT / 4; ++q)
+                s_bm4[tid * (WPT / 4) + q] = u32x4{0u, 0u, 0u, 0u};
+            __syncthreads();
+            uint32_t before = 0;
+#pragma unroll
+            for (int v = 0; v < T / kWave; ++v)
+                before += v < wave ? s_wave[v] : 0u;
+            const uint64_t g0 = cbase & ~15ull;
+            if (cend - g0 <= (uint64_t)kRkDense) {
+                // dense tile (short runs): each thread memsets its own 16 runs from
+                // registers into an LDS byte window, which leaves in 16-byte stores
+                uint8_t *s_win = reinterpret_cast<uint8_t *>(s_big4);
+                uint32_t p = (uint32_t)(cbase - g0) + before + inc - sum;
+#pragma unroll
+                for (int i = 0; i < RPT; ++i) {
+                    const uint8_t v = (uint8_t)(vv_cur[i >> 2] >> (8 * (i & 3)));
+                    const uint32_t q = p + c[i];
+                    for (; p < q; ++p)
+                        s_win[p] = v;
+                }
+                __syncthreads();
+                const uint32_t wlen = (uint32_t)(cend - g0);
+                for (uint32_t ch = tid; ch * 16 < wlen; ch += T) {
+                    const uint64_t gp = g0 + 16ull * ch;
+                    const u32x4 o = s_big4[ch];
+                    if (gp >= cbase && gp + 16 <= cend) {
+                        *reinterpret_cast<u32x4 *>(out + gp) = o;  // plain: see the note above
+                    } else {
+                        for (uint32_t f = 0; f < 16; ++f)
+                            if (gp + f >= cbase && gp + f < cend)
+                                out[gp + f] = (uint8_t)(o[f >> 2] >> (8 * (f & 3)));
+                    }
+                }
             } else {
-                for (uint32_t f = 0; f < 16; ++f)
-                    if (gp + f >= cbase && gp + f < cend)
-                        out[gp + f] = s_win[16 * ch + f];
+            {
+                uint32_t run = before + inc - sum;  // tile-local start of this thread's first run
+#pragma unroll
+                for (int i = 0; i < RPT; ++i) {
+                    s_st[tid * RPT + i] = run;
+                    run += c[i];
+                }
+                if (tid == T - 1)
+                    s_st[kRdRuns] = run;
+            }
+            const uint32_t nr = (uint32_t)(runs - tile * kRdRuns < (uint64_t)kRdRuns ? runs - tile * kRdRuns
+                                                                                      : kRdRuns);
+            __syncthreads();
+            uint32_t starts_before = 0;  // runs starting before the window
+            for (uint64_t gw = g0; gw < cend; gw += kRkWindow) {
+                // (1) start bits of the runs beginning in [gw, gw + W)
+                // (strided: lane t takes runs t, t + T, ... so a wave's ds_or targets are
+                // consecutive runs' start words -- distinct banks, not 16 words apart)
+                // Only the runs that can start in this window: runs before it are
+                // the first starts_before (counts >= 1), and starts are increasing.
+                {
+                    for (int k = (int)(starts_before / T); k < RPT; ++k) {
+                        const uint32_t j = (uint32_t)(k * T + tid);
+                        if (j >= nr)
+                            break;
+                        const uint32_t x0 = s_st[j], x1 = s_st[j + 1];
+                        const uint64_t p = cbase + x0;
+                        if (p >= gw + kRkWindow)
+                            break;
+                        if (x1 > x0 && p >= gw) {
+                            const uint32_t x = (uint32_t)(p - gw);
+                            atomicOr(&s_bm[x >> 5], 1u << (x & 31));
+                        }
+                    }
+                }
+                __syncthreads();
+                // (2) popcount prefix over the window's words; thread t owns words [WPT t, WPT t + WPT)
+                uint32_t pc[WPT];
+                uint32_t tsum = 0;
+#pragma unroll
+                for (int q = 0; q < WPT / 4; ++q) {
+                    const u32x4 w = s_bm4[tid * (WPT / 4) + q];
+#pragma unroll
+                    for (int d = 0; d < 4; ++d) {
+                        pc[q * 4 + d] = __popc(w[d]);
+                        tsum += pc[q * 4 + d];
+                    }
+                }
+                const uint32_t tinc = wave_incl_scan_u32(tsum);
+                if (lane == kWave - 1)
+                    s_wave[wave] = tinc;
+                __syncthreads();
+                uint32_t wb = 0, wtot = 0;
+#pragma unroll
+                for (int v = 0; v < T / kWave; ++v) {
+                    const uint32_t t = s_wave[v];
+                    wb += v < wave ? t : 0u;
+                    wtot += t;
+                }
+                {
+                    uint32_t run = wb + tinc - tsum;
+#pragma unroll
+                    for (int q = 0; q < WPT; ++q) {
+                        s_pre[tid * WPT + q] = run;
+                        run += pc[q];
+                    }
+                }
+                __syncthreads();
+                // (3) chunks q = k*T + tid: 16 bytes each, coalesced stores
+                const uint64_t wend = cend < gw + kRkWindow ? cend : gw + kRkWindow;
+#pragma unroll 4
+                for (int k = 0; k < CPT; ++k) {
+                    const uint32_t q = (uint32_t)(k * T + tid);
+                    const uint64_t gp = gw + 16ull * q;
+                    if (gp >= wend)
+                        break;
+                    const uint32_t word = s_bm[q >> 1];
+                    const uint32_t m = (q & 1) ? word >> 16 : word & 0xFFFFu;
+                    const uint32_t pre = s_pre[q >> 1] + ((q & 1) ? __popc(word & 0xFFFFu) : 0u);
+                    int32_t r = (int32_t)(starts_before + pre + (m & 1u)) - 1;  // run of byte 0
+                    uint32_t m1 = m & 0xFFFEu;  // starts after byte 0
+                    if (r < 0) {  // bytes before the tile's first start are not stored
+                        m1 &= m1 - 1;
+                        r = 0;
+                    }
+                    u32x4 o;
+                    if (m1 == 0) {
+                        const uint32_t s4 = (uint32_t)s_val[r] * 0x01010101u;
+                        o = u32x4{s4, s4, s4, s4};
+                    } else {
+                        // byte i takes run r + k_i, k_i = starts in bytes 1..i (<= 15): the
+                        // 16 values from run r on are gathered with byte permutes
+                        const uint32_t *v32 = reinterpret_cast<const uint32_t *>(s_val4);
+                        const uint32_t a = (uint32_t)r >> 2, sh = (uint32_t)r & 3u;
+                        const uint32_t d0 = v32[a], d1 = v32[a + 1], d2 = v32[a + 2], d3 = v32[a + 3],
+                                       d4 = v32[a + 4];
+                        const uint32_t w0 = __builtin_amdgcn_alignbyte(d1, d0, sh);
+                        const uint32_t w1 = __builtin_amdgcn_alignbyte(d2, d1, sh);
+                        const uint32_t w2 = __builtin_amdgcn_alignbyte(d3, d2, sh);
+                        const uint32_t w3 = __builtin_amdgcn_alignbyte(d4, d3, sh);
+                        constexpr uint64_t kOnes = 0x0101010101010101ull;
+                        auto spread = [](uint32_t x8) {  // bit i of x8 -> byte i (0/1)
+                            const uint64_t t = ((uint64_t)x8 * kOnes) & 0x8040201008040201ull;
+                            return ((t + 0x7F7F7F7F7F7F7F7Full) & 0x8080808080808080ull) >> 7;
+                        };
+                        const uint64_t klo = spread(m1 & 0xFFu) * kOnes;  // inclusive byte prefix
+                        const uint64_t khi = spread(m1 >> 8) * kOnes + (klo >> 56) * kOnes;
+#pragma unroll
+                        for (int d = 0; d < 4; ++d) {
+                            const uint32_t sel = (uint32_t)((d < 2 ? klo : khi) >> (32 * (d & 1)));
+                            const uint32_t lo8 = __builtin_amdgcn_perm(w1, w0, sel & 0x07070707u);
+                            const uint32_t hi8 = __builtin_amdgcn_perm(w3, w2, sel & 0x07070707u);
+                            const uint32_t hm = ((sel >> 3) & 0x01010101u) * 0xFFu;
+                            o[d] = (hi8 & hm) | (lo8 & ~hm);
+                        }
+                    }
+                    if (gp >= cbase && gp + 16 <= cend) {
+                        *reinterpret_cast<u32x4 *>(out + gp) = o;  // plain: see the note above
+                    } else {  // a chunk shared with a neighbouring tile: its bytes only
+                        for (uint32_t f = 0; f < 16; ++f)
+                            if (gp + f >= cbase && gp + f < cend)
+                                out[gp + f] = (uint8_t)(o[f >> 2] >> (8 * (f & 3)));
+                    }
+                }
+                starts_before += wtot;
+                if (gw + kRkWindow < cend) {
+                    __syncthreads();  // chunk readers of the bitmap are done
+#pragma unroll
+                    for (int q = 0; q < WPT / 4; ++q)
+                        s_bm4[tid * (WPT / 4) + q] = u32x4{0u, 0u, 0u, 0u};
+                    __syncthreads();
+                }
+            }
             }
         }
-    } else {
-    __syncthreads();
-
-    // ---- windows: the first run of a window is found by one binary search per
-    // tile, later ones are handed on by the thread whose run crosses the
-    // window end; a thread stops at the first run starting past the window
-    uint32_t ja = run_lower(s_pre, nr, 0);
-    for (uint64_t gw = g0; gw < cend; gw += kRdWindow) {
-        const uint32_t lo = (uint32_t)((gw > cbase ? gw : cbase) - cbase);  // owned, tile-local
-        const uint32_t hi = (uint32_t)((gw + kRdWindow < cend ? gw + kRdWindow : cend) - cbase);
-        const uint32_t shift = (uint32_t)(gw < cbase ? cbase - gw : 0);    // window pos of local lo
-        for (uint32_t j = ja + tid; j < nr && s_pre[j] < hi; j += kRdThreads) {
-            uint32_t x = s_pre[j], y = s_pre[j + 1];  // s_pre[nr] = the tile's total
-            if (y > hi)
-                s_next = j;  // crosses into the next window (exactly one run)
-            else if (y == hi)
-                s_next = j + 1;
-            x = x < lo ? lo : x;
-            y = y > hi ? hi : y;
-            if (x >= y)
-                continue;
-            // window positions [x - lo + shift, y - lo + shift)
-            uint32_t p = x - lo + shift, q = y - lo + shift;
-            const uint32_t v = s_val[j];
-            while (p < q && (p & 3)) s_win[p++] = (uint8_t)v;
-            const uint32_t v4 = v * 0x01010101u;
-            while (p + 4 <= q) {
-                s_win32[p >> 2] = v4;
-                p += 4;
-            }
-            while (p < q) s_win[p++] = (uint8_t)v;
-        }
-        __syncthreads();
-        ja = s_next;
-        const uint32_t wlen = (uint32_t)(cend - gw < (uint64_t)kRdWindow ? cend - gw : kRdWindow);
-        for (uint32_t ch = tid; ch * 16 < wlen; ch += kRdThreads) {
-            const uint64_t gp = gw + 16ull * ch;
-            if (gp >= cbase && gp + 16 <= cend) {
-                __builtin_nontemporal_store(s_win4[ch], reinterpret_cast<u32x4 *>(out + gp));
-            } else {
-                for (uint32_t f = 0; f < 16; ++f)
-                    if (gp + f >= cbase && gp + f < cend)
-                        out[gp + f] = s_win[16 * ch + f];
-            }
-        }
-        __syncthreads();
-    }
-    }
-    }
-    if (next >= ntiles)
-        break;
-    tile = next;
+        if (next >= ntiles)
+            break;
+        tile = next;
     }
 }
+
 
 struct RlEncLayout {
     size_t tiles, bytes;
