@@ -59,7 +59,7 @@ struct WVec<4> {
     typedef uint32_t T;
 };
 
-template <int T, int ITEMS>
+template <int T, int ITEMS, int NTL = 1>
 __device__ __forceinline__ void load_vals(u32x4 (&a)[ITEMS], const uint8_t *values, uint64_t base,
                                           uint32_t agg, uint64_t vsize)
 {
@@ -69,7 +69,7 @@ __device__ __forceinline__ void load_vals(u32x4 (&a)[ITEMS], const uint8_t *valu
 #pragma unroll
         for (int k = 0; k < ITEMS; ++k)
             if ((uint32_t)(k * T + tid) < agg)
-                a[k] = __builtin_nontemporal_load(src + k * T + tid);
+                a[k] = NTL ? __builtin_nontemporal_load(src + k * T + tid) : src[k * T + tid];
     } else {
 #pragma unroll
         for (int k = 0; k < ITEMS; ++k)
@@ -198,7 +198,7 @@ __global__ __launch_bounds__(T, BPC) void dec_p(const uint8_t *__restrict__ bits
 }
 
 // PT: P with tiles taken by ticket (in-order progress across workgroups)
-template <int T, int ITEMS, int BPC>
+template <int T, int ITEMS, int BPC, int NTS = 1, int NTL = 1>
 __global__ __launch_bounds__(T, BPC) void dec_pt(const uint8_t *__restrict__ bits, uint64_t nframes,
                                                 const uint8_t *__restrict__ values, uint64_t vsize,
                                                 uint8_t *__restrict__ out, uint64_t n,
@@ -223,7 +223,7 @@ __global__ __launch_bounds__(T, BPC) void dec_pt(const uint8_t *__restrict__ bit
     uint64_t base = tbase(tile);
     uint32_t agg = (uint32_t)(tbase(tile + 1) - base);
     u32x4 a[ITEMS];
-    load_vals<T, ITEMS>(a, values, base, agg, vsize);
+    load_vals<T, ITEMS, NTL>(a, values, base, agg, vsize);
     typename WVec<ITEMS>::T wv = load_w<ITEMS>(bits, (uint64_t)tile * TF + (tid >> 3) * ITEMS, nframes);
     for (;;) {
         if (tid == 0)
@@ -259,7 +259,7 @@ __global__ __launch_bounds__(T, BPC) void dec_pt(const uint8_t *__restrict__ bit
         if (more) {
             base = tbase(nxt);
             agg = (uint32_t)(tbase(nxt + 1) - base);
-            load_vals<T, ITEMS>(a, values, base, agg, vsize);
+            load_vals<T, ITEMS, NTL>(a, values, base, agg, vsize);
             wv = load_w<ITEMS>(bits, (uint64_t)nxt * TF + (tid >> 3) * ITEMS, nframes);
         }
         // unpack + store
@@ -288,7 +288,10 @@ __global__ __launch_bounds__(T, BPC) void dec_pt(const uint8_t *__restrict__ bit
             const uint64_t x1 = unpack8(p1, b);
             const u32x4 r = u32x4{(uint32_t)x0, (uint32_t)(x0 >> 32), (uint32_t)x1, (uint32_t)(x1 >> 32)};
             if (full)
-                __builtin_nontemporal_store(r, reinterpret_cast<u32x4 *>(dst + k * kFrame));
+                if (NTS)
+                    __builtin_nontemporal_store(r, reinterpret_cast<u32x4 *>(dst + k * kFrame));
+                else
+                    *reinterpret_cast<u32x4 *>(dst + k * kFrame) = r;
             else
                 store16_tail(out, (uint64_t)(dst - out) + k * kFrame, n, r);
         }
@@ -759,7 +762,7 @@ static void run_f(const Ctx &c, hipStream_t s, int cus)
                        reinterpret_cast<uint64_t *>(g_fscr.p + 16));
 }
 
-template <int T, int ITEMS, int BPC>
+template <int T, int ITEMS, int BPC, int NTS = 1, int NTL = 1>
 static void run_pt(const Ctx &c, hipStream_t s, int cus)
 {
     constexpr int TB = T * 16 * ITEMS;
@@ -770,7 +773,7 @@ static void run_pt(const Ctx &c, hipStream_t s, int cus)
         g_fscr.bytes = 1 << 20;
     }
     CK(hipMemsetAsync(g_fscr.p, 0, 16, s));
-    hipLaunchKernelGGL((dec_pt<T, ITEMS, BPC>), dim3(grid), dim3(T), 0, s, c.d_bits, (uint64_t)c.frames,
+    hipLaunchKernelGGL((dec_pt<T, ITEMS, BPC, NTS, NTL>), dim3(grid), dim3(T), 0, s, c.d_bits, (uint64_t)c.frames,
                        c.d_vals, (uint64_t)c.vsize, c.d_out, (uint64_t)c.n, c.tb32, (uint32_t)(TB / 16384),
                        c.ntb32, ntiles, reinterpret_cast<Ctrl *>(g_fscr.p));
 }
@@ -858,18 +861,16 @@ int main(int argc, char **argv)
              flrl_fl_decode_device(c.d_bits, c.frames, c.d_vals, c.vsize, c.d_out, c.n, c.d_scr, c.scr_b, s);
          }},
         {"NP<8,0> 32K (lib kernel)", run_np<8, 0>},
-        {"NP<16,1> 64K DMA", run_np<16, 1>},
-        {"P<256,8,4> 32K", run_p<256, 8, 4>},
-        {"PT<1024,8,1> 128K ticket", run_pt<1024, 8, 1>},
-        {"PT<512,16,1> 128K ticket", run_pt<512, 16, 1>},
-        {"PT<512,4,4> 32K ticket", run_pt<512, 4, 4>},
+        {"PT<512,8,2> plain stores", run_pt<512, 8, 2, 0, 1>},
+        {"PT<512,8,2> plain loads", run_pt<512, 8, 2, 1, 0>},
+        {"PT<512,8,2> plain both", run_pt<512, 8, 2, 0, 0>},
         {"PT<512,8,2> 64K ticket", run_pt<512, 8, 2>},
         {"copy U4 x8", run_copy<4, 8>},
         {"copy U8 x4", run_copy<8, 4>},
         {"copy U16 x1", run_copy<16, 1>},
     };
     const int nv = sizeof(vars) / sizeof(vars[0]);
-    for (int v = 1; v + 4 < nv; ++v) {
+    for (int v = 1; v + 3 < nv; ++v) {
         CK(hipMemsetAsync(c.d_out, 0xA5, n, s));
         vars[v].fn(c, s, cus);
         if (check(c, vars[v].name))
