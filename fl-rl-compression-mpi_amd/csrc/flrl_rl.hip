@@ -587,7 +587,12 @@ __global__ __launch_bounds__(T) void rl_encode_kernel(
     // ---- one look-back: (heads before the tile, chunk state at its start) --
     if (w == 0) {
         const uint64_t tmap = first != 0xFFFFFFFFu ? sm_nat(first, K, rel_in & 0xFFu) : sm_nonat(tile_len);
+#ifdef FLRL_RL_NO_LOOKBACK  // timing ablation only (scripts/ubench_rl.hip): wrong output
+        const uint64_t state = (((uint64_t)tile * 4000ull) << 8) | 1u;
+        (void)tmap;
+#else
         const uint64_t state = lookback_seg<kRlLookG>(status, tile, tmap, ctrl);
+#endif
         FLRL_RL_TRACE(tile, 4);
         if (lane == 0)
             *s_state = state;
