@@ -173,7 +173,9 @@ __global__ __launch_bounds__(T + kWave, 1) void fl_encode_kernel(
     // wave T/64 (the look-back wave) holds no tile data: it publishes and
     // resolves the look-back while the T data threads pack and prefetch
     const bool lw = tid >= T;
-    if (tid == 0)
+    // tickets are taken by the look-back wave too: it has no bulk loads or
+    // stores in flight, so waiting for the atomic's return costs no drain
+    if (tid == T)
         s_next = atomicAdd(&ctrl->ticket, 1u);
     __syncthreads();
     uint32_t tile = s_next;
@@ -187,7 +189,7 @@ __global__ __launch_bounds__(T + kWave, 1) void fl_encode_kernel(
         // no barrier here: s_out/s_w of the previous tile are re-written only
         // after the widths barrier below, which every wave reaches after its
         // stores; s_next was read by all before the previous look-back barrier
-        if (tid == 0)
+        if (tid == T)
             s_next = atomicAdd(&ctrl->ticket, 1u);  // next ticket, read after the barrier below
         FLRL_FL_TRACE(tile, 0);
         const uint64_t frame0 = (uint64_t)tile * TF;

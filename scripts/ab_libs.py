@@ -1,0 +1,119 @@
+#!/usr/bin/env python3
+"""A/B two (or more) builds of libflrl.so in ONE process on the same device
+buffers: each library is loaded by path with ctypes (separate code objects,
+one HIP runtime), the chosen device entry point is timed with HIP events,
+builds interleaved rep by rep, and every build's output is checked against the
+first's. Usage (on the GPU box):
+
+  python scripts/ab_libs.py --op fl_encode --libs scripts/ab_libs/libflrl_old.so,fl-rl-compression-mpi_amd/lib/libflrl.so
+
+ops: fl_encode, fl_decode, rl_encode, rl_decode. Inputs: --kind u8|lo4|zero
+(device generator) or runs32|longruns (host generator), --bytes (default 1 GiB).
+"""
+import argparse
+import ctypes
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "fl-rl-compression-mpi_amd"))
+import torch  # noqa: E402
+
+import flrl  # noqa: E402
+from flrl.device import FLDevice, RLDevice, gen  # noqa: E402
+
+VP, SZ = ctypes.c_void_p, ctypes.c_size_t
+
+
+def load(path):
+    lib = ctypes.CDLL(os.path.abspath(path))
+    lib.flrl_fl_encode_device.argtypes = [VP, SZ, VP, VP, VP, VP, SZ, VP]
+    lib.flrl_fl_decode_device.argtypes = [VP, SZ, VP, SZ, VP, SZ, VP, SZ, VP]
+    lib.flrl_rl_encode_device.argtypes = [VP, SZ, VP, VP, VP, VP, SZ, VP]
+    lib.flrl_rl_decode_device.argtypes = [VP, VP, SZ, VP, SZ, VP, SZ, VP]
+    for f in ("flrl_fl_encode_device", "flrl_fl_decode_device", "flrl_rl_encode_device",
+              "flrl_rl_decode_device"):
+        getattr(lib, f).restype = ctypes.c_int
+    return lib
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--op", default="fl_encode", choices=["fl_encode", "fl_decode", "rl_encode", "rl_decode"])
+    p.add_argument("--libs", required=True)
+    p.add_argument("--kind", default="")
+    p.add_argument("--bytes", type=int, default=1 << 30)
+    p.add_argument("--reps", type=int, default=20)
+    a = p.parse_args()
+    libs = [load(x) for x in a.libs.split(",")]
+    n = a.bytes
+    kind = a.kind or ("runs32" if a.op.startswith("rl") else "u8")
+    x = (gen(kind, n, 42) if kind in ("u8", "lo4", "zero")
+         else torch.from_numpy(flrl.gen_host(kind, n, 42)).cuda())
+    s = torch.cuda.current_stream().cuda_stream
+    if a.op.startswith("fl"):
+        d = FLDevice(n, "cuda")
+        d.encode(x)
+        V = d.values_size()
+
+        def call(lib):
+            if a.op == "fl_encode":
+                return lib.flrl_fl_encode_device(x.data_ptr(), n, d.bits.data_ptr(), d.values.data_ptr(),
+                                                 d.sizes.data_ptr() + 8, d.scratch.data_ptr(),
+                                                 d.scratch_bytes, s)
+            return lib.flrl_fl_decode_device(d.bits.data_ptr(), d.frames, d.values.data_ptr(), V,
+                                             d.out.data_ptr(), n, d.scratch.data_ptr(), d.scratch_bytes, s)
+
+        def result():
+            if a.op == "fl_encode":
+                return torch.cat([d.bits[: d.frames], d.values[: d.values_size()]])
+            return d.out[:n].clone()
+        alg = n + d.frames + V
+    else:
+        d = RLDevice(n, "cuda")
+        d.encode(x)
+        R = d.runs()
+
+        def call(lib):
+            if a.op == "rl_encode":
+                return lib.flrl_rl_encode_device(x.data_ptr(), n, d.counts.data_ptr(), d.values.data_ptr(),
+                                                 d.runs_t.data_ptr(), d.scratch.data_ptr(), d.scratch_bytes, s)
+            return lib.flrl_rl_decode_device(d.counts.data_ptr(), d.values.data_ptr(), R, d.out.data_ptr(), n,
+                                             d.scratch.data_ptr(), d.scratch_bytes, s)
+
+        def result():
+            if a.op == "rl_encode":
+                r = d.runs()
+                return torch.cat([d.counts[:r], d.values[:r]])
+            return d.out[:n].clone()
+        alg = n + 2 * R
+    ref = None
+    for i, lib in enumerate(libs):
+        assert call(lib) == 0, flrl.last_error() if hasattr(flrl, "last_error") else "call failed"
+        torch.cuda.synchronize()
+        assert d.error() == 0
+        r = result()
+        if ref is None:
+            ref = r
+            if a.op.endswith("decode"):
+                assert torch.equal(r, x[:n]), "round trip failed"
+        else:
+            assert torch.equal(ref, r), f"build {i} output differs from build 0"
+    print(f"{a.op} {kind} n={n}: outputs of {len(libs)} builds identical", flush=True)
+    tot = [0.0] * len(libs)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for r in range(a.reps):
+        for i, lib in enumerate(libs):
+            e0.record()
+            call(lib)
+            e1.record()
+            e1.synchronize()
+            if r:
+                tot[i] += e0.elapsed_time(e1)
+    for i, path in enumerate(a.libs.split(",")):
+        ms = tot[i] / (a.reps - 1)
+        print(f"  {os.path.basename(path):24s} {ms:.4f} ms  {alg / ms / 1e6:.1f} GB/s alg", flush=True)
+
+
+if __name__ == "__main__":
+    main()
