@@ -153,3 +153,40 @@ def test_device_1gib_runs32():
     out = d.decode(R)
     assert d.error() == 0
     assert torch.equal(out, x)
+
+
+# ---- rank decode: dense-path threshold (tile output <= 32 KiB), 64 KiB
+# windows, chunks with 0..16 run starts, tiles starting mid-chunk -------------
+@pytest.mark.parametrize("runlen", [7, 8, 9, 15, 16, 17, 24, 31, 33, 63, 64])
+def test_decode_fixed_run_lengths(runlen):
+    # every tile of 4096 runs has output 4096 * runlen: at, below and above the
+    # dense threshold (8) and the 64 KiB window (16); run starts fall at every
+    # offset within 16-byte chunks when runlen is odd
+    nruns = 3 * 4096 + 77
+    vals = (np.arange(nruns) * 37 % 251 + 1).astype(np.uint8)
+    a = np.repeat(vals, runlen)
+    check(a[: a.size - 3])
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_decode_mixed_tile_densities(seed):
+    # tiles alternate between dense (runs of 1..4) and sparse (runs of 20..200)
+    # stretches, so neighbouring tiles take different decode paths and a
+    # window's first chunk is shared with a tile of the other kind
+    rng = np.random.default_rng(seed)
+    parts = []
+    for k in range(24):
+        lo, hi = (1, 5) if k % 2 == 0 else (20, 201)
+        lens = rng.integers(lo, hi, size=int(rng.integers(1000, 9000)))
+        vals = (np.cumsum(rng.integers(1, 255, size=lens.size)) % 256).astype(np.uint8)
+        parts.append(np.repeat(vals, lens))
+    check(np.concatenate(parts))
+
+
+def test_decode_all_starts_in_chunk():
+    # runs of exactly 1 byte for whole tiles (16 starts per chunk), then runs of
+    # 2 and 3 (8 and 5-6 starts), in one input
+    a = np.concatenate([(np.arange(70_000) % 2).astype(np.uint8),
+                        np.repeat((np.arange(40_000) % 2 + 5).astype(np.uint8), 2),
+                        np.repeat((np.arange(40_000) % 3 + 9).astype(np.uint8), 3)])
+    check(a)
