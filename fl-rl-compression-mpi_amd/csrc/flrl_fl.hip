@@ -162,7 +162,7 @@ __global__ __launch_bounds__(T + kWave, 1) void fl_encode_kernel(
     __shared__ u32x4 s_out[TB / 16];
     __shared__ u32x4 s_w4[TF / 16];
     __shared__ uint32_t s_wave[T / kWave];
-    __shared__ uint32_t s_next;
+    __shared__ uint32_t s_next[2];  // alternating: a slot is rewritten two barriers after its read
     __shared__ uint64_t s_base;
     static_assert(ITEMS == 16, "a lane group's 16 frame widths are one 16-byte vector");
     uint8_t *s_w = reinterpret_cast<uint8_t *>(s_w4);
@@ -176,11 +176,12 @@ __global__ __launch_bounds__(T + kWave, 1) void fl_encode_kernel(
     // tickets are taken by the look-back wave too: it has no bulk loads or
     // stores in flight, so waiting for the atomic's return costs no drain
     if (tid == T)
-        s_next = atomicAdd(&ctrl->ticket, 1u);
+        s_next[0] = atomicAdd(&ctrl->ticket, 1u);
     __syncthreads();
-    uint32_t tile = s_next;
+    uint32_t tile = s_next[0];
     if (tile >= ntiles)
         return;
+    uint32_t slot = 1;
     u32x4 a[ITEMS];
     if (!lw)
         load_tile_g<T, ITEMS>(a, in, (uint64_t)tile * TB, n);
@@ -188,9 +189,10 @@ __global__ __launch_bounds__(T + kWave, 1) void fl_encode_kernel(
     for (;;) {
         // no barrier here: s_out/s_w of the previous tile are re-written only
         // after the widths barrier below, which every wave reaches after its
-        // stores; s_next was read by all before the previous look-back barrier
+        // stores; s_next[slot] was last read two barriers ago (the initial
+        // ticket: before the widths barrier of the first tile)
         if (tid == T)
-            s_next = atomicAdd(&ctrl->ticket, 1u);  // next ticket, read after the barrier below
+            s_next[slot] = atomicAdd(&ctrl->ticket, 1u);  // next ticket, read after the barrier below
         FLRL_FL_TRACE(tile, 0);
         const uint64_t frame0 = (uint64_t)tile * TF;
 
@@ -223,7 +225,8 @@ __global__ __launch_bounds__(T + kWave, 1) void fl_encode_kernel(
                 s_w4[tid >> 3] = wv;
         }
         __syncthreads();
-        const uint32_t nxt = s_next;
+        const uint32_t nxt = s_next[slot];
+        slot ^= 1u;
         uint32_t wbase = 0, agg = 0;
 #pragma unroll
         for (int v = 0; v < T / kWave; ++v) {

@@ -302,6 +302,117 @@ __global__ __launch_bounds__(T, BPC) void dec_pt(const uint8_t *__restrict__ bit
     }
 }
 
+template <int T, int ITEMS, int BPC, int NTS = 1, int NTL = 1>
+// PAIR: one ticket = two consecutive tiles (half the atomics)
+__global__ __launch_bounds__(T, BPC) void dec_pt2(const uint8_t *__restrict__ bits, uint64_t nframes,
+                                                const uint8_t *__restrict__ values, uint64_t vsize,
+                                                uint8_t *__restrict__ out, uint64_t n,
+                                                const uint64_t *__restrict__ tb, uint32_t stride,
+                                                uint32_t ntb, uint32_t ntiles, Ctrl *ctrl)
+{
+    constexpr int TB = T * 16 * ITEMS;
+    constexpr int TF = TB / kFrame;
+    __shared__ u32x4 s_in[TB / 16 + 2];
+    __shared__ uint32_t s_wave[T / kWave];
+    const int tid = threadIdx.x;
+    const int lane = tid & (kWave - 1);
+    const int wave = tid / kWave;
+    __shared__ uint32_t s_next;
+    if (tid == 0)
+        s_next = 2u * atomicAdd(&ctrl->ticket, 1u);
+    __syncthreads();
+    uint32_t tile = s_next;
+    uint32_t pending = tile + 1;
+    bool have = true;
+    if (tile >= ntiles)
+        return;
+    auto tbase = [&](uint32_t t) { return tb[(uint64_t)t * stride < ntb ? (uint64_t)t * stride : ntb]; };
+    uint64_t base = tbase(tile);
+    uint32_t agg = (uint32_t)(tbase(tile + 1) - base);
+    u32x4 a[ITEMS];
+    load_vals<T, ITEMS, NTL>(a, values, base, agg, vsize);
+    typename WVec<ITEMS>::T wv = load_w<ITEMS>(bits, (uint64_t)tile * TF + (tid >> 3) * ITEMS, nframes);
+    for (;;) {
+        if (tid == 0)
+            if (!have)
+                s_next = 2u * atomicAdd(&ctrl->ticket, 1u);  // read after the scan barrier
+#pragma unroll
+        for (int k = 0; k < ITEMS; ++k)
+            if ((uint32_t)(k * T + tid) < agg)
+                s_in[k * T + tid] = a[k];
+        if (tid < 2)
+            s_in[agg + tid] = u32x4{0u, 0u, 0u, 0u};
+        uint32_t bw[ITEMS];
+        uint32_t gtot = 0;
+#pragma unroll
+        for (int k = 0; k < ITEMS; ++k) {
+            uint32_t b = wbyte<ITEMS>(wv, k);
+            const uint64_t f = (uint64_t)tile * TF + (tid >> 3) * ITEMS + k;
+            b = f < nframes ? clamp_width(b) : 0u;
+            bw[k] = b;
+            gtot += b;
+        }
+        const uint32_t gincl = wave_incl_scan_u32((lane & 7) == 0 ? gtot : 0u);
+        if (lane == kWave - 1)
+            s_wave[wave] = gincl;
+        __syncthreads();
+        uint32_t wbase = 0;
+#pragma unroll
+        for (int v = 0; v < T / kWave; ++v)
+            wbase += v < wave ? s_wave[v] : 0u;
+        // prefetch the next tile
+        const uint32_t nxt = have ? pending : s_next;
+        if (!have)
+            pending = nxt + 1;
+        have = !have;
+        const bool more = nxt < ntiles;
+        const uint64_t tile_off = (uint64_t)tile * TB;
+        if (more) {
+            base = tbase(nxt);
+            agg = (uint32_t)(tbase(nxt + 1) - base);
+            load_vals<T, ITEMS, NTL>(a, values, base, agg, vsize);
+            wv = load_w<ITEMS>(bits, (uint64_t)nxt * TF + (tid >> 3) * ITEMS, nframes);
+        }
+        // unpack + store
+        const uint32_t *s32 = reinterpret_cast<const uint32_t *>(s_in);
+        const bool full = tile_off + TB <= n;
+        uint32_t run = wbase + gincl - gtot;
+        uint8_t *dst = out + tile_off + (uint32_t)(tid >> 3) * ITEMS * kFrame + (tid & 7) * 16;
+#pragma unroll
+        for (int k = 0; k < ITEMS; ++k) {
+            const uint32_t b = bw[k];
+            const uint32_t off = 16u * run + 2u * b * (uint32_t)(tid & 7);
+            run += b;
+            if (b == 0)
+                continue;
+            const uint32_t ad = off >> 2;
+            const uint64_t w01 = ((uint64_t)s32[ad + 1] << 32) | s32[ad];
+            const uint64_t w23 = ((uint64_t)s32[ad + 3] << 32) | s32[ad + 2];
+            uint64_t lo = w01, hi = w23;
+            if (off & 2) {
+                const uint64_t w4 = s32[ad + 4];
+                lo = (w01 >> 16) | (w23 << 48);
+                hi = (w23 >> 16) | (w4 << 48);
+            }
+            const uint64_t p1 = b == 8 ? hi : ((lo >> (8 * b)) | (hi << (64 - 8 * b)));
+            const uint64_t x0 = unpack8(lo, b);
+            const uint64_t x1 = unpack8(p1, b);
+            const u32x4 r = u32x4{(uint32_t)x0, (uint32_t)(x0 >> 32), (uint32_t)x1, (uint32_t)(x1 >> 32)};
+            if (full)
+                if (NTS)
+                    __builtin_nontemporal_store(r, reinterpret_cast<u32x4 *>(dst + k * kFrame));
+                else
+                    *reinterpret_cast<u32x4 *>(dst + k * kFrame) = r;
+            else
+                store16_tail(out, (uint64_t)(dst - out) + k * kFrame, n, r);
+        }
+        if (!more)
+            break;
+        tile = nxt;
+        __syncthreads();  // LDS reuse
+    }
+}
+
 // Non-persistent (the library's shape): one 256-thread workgroup per
 // 16*256*ITEMS-byte output tile; DMA = packed bytes by LDS-DMA instead of
 // load -> VGPR -> ds_write.
@@ -762,6 +873,22 @@ static void run_f(const Ctx &c, hipStream_t s, int cus)
                        reinterpret_cast<uint64_t *>(g_fscr.p + 16));
 }
 
+template <int T, int ITEMS, int BPC, int PAIR = 0>
+static void run_pt2(const Ctx &c, hipStream_t s, int cus)
+{
+    constexpr int TB = T * 16 * ITEMS;
+    const uint32_t ntiles = (uint32_t)((c.n + TB - 1) / TB);
+    const uint32_t grid = std::min<uint32_t>((ntiles + 1) / 2, (uint32_t)cus * BPC);
+    if (!g_fscr.p) {
+        CK(hipMalloc(&g_fscr.p, 1 << 20));
+        g_fscr.bytes = 1 << 20;
+    }
+    CK(hipMemsetAsync(g_fscr.p, 0, 16, s));
+    hipLaunchKernelGGL((dec_pt2<T, ITEMS, BPC>), dim3(grid), dim3(T), 0, s, c.d_bits, (uint64_t)c.frames,
+                       c.d_vals, (uint64_t)c.vsize, c.d_out, (uint64_t)c.n, c.tb32, (uint32_t)(TB / 16384),
+                       c.ntb32, ntiles, reinterpret_cast<Ctrl *>(g_fscr.p));
+}
+
 template <int T, int ITEMS, int BPC, int NTS = 1, int NTL = 1>
 static void run_pt(const Ctx &c, hipStream_t s, int cus)
 {
@@ -861,9 +988,8 @@ int main(int argc, char **argv)
              flrl_fl_decode_device(c.d_bits, c.frames, c.d_vals, c.vsize, c.d_out, c.n, c.d_scr, c.scr_b, s);
          }},
         {"NP<8,0> 32K (lib kernel)", run_np<8, 0>},
-        {"PT<512,8,2> plain stores", run_pt<512, 8, 2, 0, 1>},
-        {"PT<512,8,2> plain loads", run_pt<512, 8, 2, 1, 0>},
-        {"PT<512,8,2> plain both", run_pt<512, 8, 2, 0, 0>},
+        {"PT2<512,8,2> pair tickets", run_pt2<512, 8, 2>},
+        {"PT2<256,8,4> 32K pair tickets", run_pt2<256, 8, 4>},
         {"PT<512,8,2> 64K ticket", run_pt<512, 8, 2>},
         {"copy U4 x8", run_copy<4, 8>},
         {"copy U8 x4", run_copy<8, 4>},

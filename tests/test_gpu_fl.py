@@ -253,6 +253,36 @@ def test_device_decode_offsets_rounds():
     torch.cuda.empty_cache()
 
 
+@pytest.mark.parametrize("kind", ["u8", "lo4"])
+def test_device_repeat_stability(kind):
+    """Back-to-back device encodes/decodes of the same 96 MiB + 77 input, every
+    output compared with the first: persistent workgroups, tickets and LDS
+    hand-offs must give identical results on every launch (catches
+    intra-workgroup races on shared ticket/base slots)."""
+    from flrl.device import FLDevice, gen
+    n = (96 << 20) + 77
+    x = gen(kind, n, 9)
+    d = FLDevice(n)
+    d.encode(x)
+    v = d.values_size()
+    bits0, vals0 = d.bits[: d.frames].clone(), d.values[:v].clone()
+    out = torch.empty_like(x)
+    for _ in range(30):
+        d.encode(x)
+        d.decode(v, out=out)
+    torch.cuda.synchronize()
+    assert d.error() == 0 and d.values_size() == v
+    for i in range(30):
+        d.encode(x)
+        assert torch.equal(d.bits[: d.frames], bits0) and torch.equal(d.values[:v], vals0), i
+        out.zero_()
+        d.decode(v, out=out)
+        assert torch.equal(out[:n], x[:n]), i
+    assert d.error() == 0
+    del d, x, out
+    torch.cuda.empty_cache()
+
+
 # ------------------------------------------------------------------ sharded
 def test_sharded_equals_single(bmp_bytes):
     ng = flrl.device_count()
