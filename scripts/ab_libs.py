@@ -8,7 +8,8 @@ first's. Usage (on the GPU box):
   python scripts/ab_libs.py --op fl_encode --libs scripts/ab_libs/libflrl_old.so,fl-rl-compression-mpi_amd/lib/libflrl.so
 
 ops: fl_encode, fl_decode, rl_encode, rl_decode. Inputs: --kind u8|lo4|zero
-(device generator) or runs32|longruns (host generator), --bytes (default 1 GiB).
+(device generator), runs32|longruns (host generator) or uptoM (uniform runs of
+1..M bytes), --bytes (default 1 GiB).
 """
 import argparse
 import ctypes
@@ -48,8 +49,17 @@ def main():
     libs = [load(x) for x in a.libs.split(",")]
     n = a.bytes
     kind = a.kind or ("runs32" if a.op.startswith("rl") else "u8")
-    x = (gen(kind, n, 42) if kind in ("u8", "lo4", "zero")
-         else torch.from_numpy(flrl.gen_host(kind, n, 42)).cuda())
+    if kind in ("u8", "lo4", "zero"):
+        x = gen(kind, n, 42)
+    elif kind.startswith("upto"):  # uniform run lengths 1..M (M = the number after "upto")
+        import numpy as np
+        rng = np.random.default_rng(42)
+        m = int(kind[4:])
+        lens = rng.integers(1, m + 1, size=int(2.2 * n / (m + 1)) + 4096)
+        vals = (np.cumsum(rng.integers(1, 255, size=lens.size)) % 256).astype(np.uint8)
+        x = torch.from_numpy(np.repeat(vals, lens)[:n].copy()).cuda()
+    else:
+        x = torch.from_numpy(flrl.gen_host(kind, n, 42)).cuda()
     s = torch.cuda.current_stream().cuda_stream
     if a.op.startswith("fl"):
         d = FLDevice(n, "cuda")
