@@ -346,6 +346,11 @@ __global__ __launch_bounds__(kThreads) void fl_offsets_kernel(
     const int lane = tid & (kWave - 1);
     const int wave = tid / kWave;
     const uint32_t blk = take_ticket(ctrl, &s_ticket);
+    if (blk >= nblocks) {  // the scratch's ticket was not reset for this launch
+        if (threadIdx.x == 0)
+            raise_error(ctrl, FLRL_E_ARG);
+        return;
+    }
     uint64_t local = 0;          // frames' 16-byte units before this round, workgroup-relative
     bool has_last = false;       // this lane holds the last frame
     uint64_t last_local = 0;     // its units before the last frame, workgroup-relative

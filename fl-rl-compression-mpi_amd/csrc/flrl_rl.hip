@@ -348,6 +348,11 @@ __global__ __launch_bounds__(T) void rl_encode_kernel(
     const uint8_t *my = img + o;
     FLRL_RL_PHASE_BEGIN();
     const uint32_t tile = take_ticket(ctrl, s_ticket);
+    if (tile >= ntiles) {  // the scratch's ticket was not reset for this launch
+        if (threadIdx.x == 0)
+            raise_error(ctrl, FLRL_E_ARG);
+        return;
+    }
     FLRL_RL_TRACE(tile, 0);
     const uint64_t tile_off = (uint64_t)tile * (SUB * TB);
     const uint32_t tile_len = (uint32_t)(n - tile_off < (uint64_t)(SUB * TB) ? n - tile_off : SUB * TB);
@@ -742,6 +747,11 @@ __global__ __launch_bounds__(kThreads) void rl_offsets_kernel(
     const int lane = tid & (kWave - 1);
     const int wave = tid / kWave;
     const uint32_t blk = take_ticket(ctrl, &s_ticket);
+    if (blk >= nblocks) {  // the scratch's ticket was not reset for this launch
+        if (threadIdx.x == 0)
+            raise_error(ctrl, FLRL_E_ARG);
+        return;
+    }
     constexpr int kLanesPerTile = kRdRuns / kRoRunsPerThread;
     uint64_t local = 0;  // output bytes before this round, workgroup-relative
     bool bad = false;
