@@ -862,6 +862,7 @@ __global__ __launch_bounds__(kRdThreads) void rl_decode_kernel(
     __shared__ u32x4 s_big4[(2 * kRkWords + kRdRuns + 1 + 3) / 4];
     __shared__ u32x4 s_val4[kRdRuns / 16 + 1];  // +16 B: the permute window reads up to 19 bytes past a run
     __shared__ uint32_t s_wave[T / kWave];
+    __shared__ uint64_t s_pfx[256];  // byte i of s_pfx[x] = popcount(x & ((2 << i) - 1))
     static_assert(sizeof(s_big4) >= kRkDense, "dense window fits the aliased LDS");
     u32x4 *const s_bm4 = s_big4;
     uint32_t *const s_bm = reinterpret_cast<uint32_t *>(s_big4);
@@ -875,6 +876,17 @@ __global__ __launch_bounds__(kRdThreads) void rl_decode_kernel(
     uint64_t tile = blockIdx.x;
     if (tile >= ntiles)
         return;
+    {
+        static_assert(T == 256, "one table entry per thread");
+        uint64_t e = 0;
+        uint32_t c = 0;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            c += (tid >> i) & 1;
+            e |= (uint64_t)c << (8 * i);
+        }
+        s_pfx[tid] = e;  // read after the first tile's barriers
+    }
     u32x4 cv = load16_tail(counts, tile * kRdRuns + tid * RPT, runs);
     u32x4 vv = load16_tail(values, tile * kRdRuns + tid * RPT, runs);
     uint64_t base = tile_base[tile], end = tile_base[tile + 1];
@@ -1037,19 +1049,18 @@ __global__ __launch_bounds__(kRdThreads) void rl_decode_kernel(
                         const uint32_t w1 = __builtin_amdgcn_alignbyte(d2, d1, sh);
                         const uint32_t w2 = __builtin_amdgcn_alignbyte(d3, d2, sh);
                         const uint32_t w3 = __builtin_amdgcn_alignbyte(d4, d3, sh);
-                        constexpr uint64_t kOnes = 0x0101010101010101ull;
-                        auto spread = [](uint32_t x8) {  // bit i of x8 -> byte i (0/1)
-                            const uint64_t t = ((uint64_t)x8 * kOnes) & 0x8040201008040201ull;
-                            return ((t + 0x7F7F7F7F7F7F7F7Full) & 0x8080808080808080ull) >> 7;
-                        };
-                        const uint64_t klo = spread(m1 & 0xFFu) * kOnes;  // inclusive byte prefix
-                        const uint64_t khi = spread(m1 >> 8) * kOnes + (klo >> 56) * kOnes;
+                        // k_i as bytes: s_pfx[x] byte i = popcount of x's bits 0..i (a table:
+                        // no 64-bit multiplies); the high half adds the low byte's total
+                        const uint64_t klo = s_pfx[m1 & 0xFFu];
+                        const uint32_t plo = (uint32_t)__popc(m1 & 0xFFu) * 0x01010101u;
+                        const uint64_t khi = s_pfx[m1 >> 8] + (((uint64_t)plo << 32) | plo);
 #pragma unroll
                         for (int d = 0; d < 4; ++d) {
                             const uint32_t sel = (uint32_t)((d < 2 ? klo : khi) >> (32 * (d & 1)));
                             const uint32_t lo8 = __builtin_amdgcn_perm(w1, w0, sel & 0x07070707u);
                             const uint32_t hi8 = __builtin_amdgcn_perm(w3, w2, sel & 0x07070707u);
-                            const uint32_t hm = ((sel >> 3) & 0x01010101u) * 0xFFu;
+                            const uint32_t h1 = (sel >> 3) & 0x01010101u;
+                            const uint32_t hm = (h1 << 8) - h1;  // 0xFF where k_i >= 8
                             o[d] = (hi8 & hm) | (lo8 & ~hm);
                         }
                     }
