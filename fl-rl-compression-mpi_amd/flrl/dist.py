@@ -37,9 +37,9 @@ def size_scan(sizes: torch.Tensor, group=None) -> tuple[torch.Tensor, torch.Tens
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     sizes = sizes.reshape(2).to(torch.int64)
-    parts = [torch.empty_like(sizes) for _ in range(world)]
-    dist.all_gather(parts, sizes, group=group)
-    allsz = torch.stack(parts)               # [world, 2]
+    flat = torch.empty(world * 2, dtype=torch.int64, device=sizes.device)
+    dist.all_gather_into_tensor(flat, sizes, group=group)  # one buffer: no per-rank list + stack
+    allsz = flat.view(world, 2)
     incl = torch.cumsum(allsz, dim=0)
     excl = incl - allsz
     return excl[rank], incl[-1]
