@@ -626,10 +626,12 @@ __global__ __launch_bounds__(T) void rl_encode_kernel(
                 counts[g0 - 1] = (uint8_t)(c == 0 ? 255u : c);
                 values[g0 - 1] = tsv[0];
             }
+#ifndef FLRL_RL_NO_EMIT  // timing ablation only (scripts/ubench_rl.hip): wrong output
             for (uint32_t j = 1 + (uint32_t)tid; j < Kst; j += T) {
                 counts[g0 + j - 1] = tsc[j];
                 values[g0 + j - 1] = tsv[j];
             }
+#endif
         }
     }
     if (nst < ns) {
