@@ -74,6 +74,21 @@ def file_sha(n, frames, bits: np.ndarray, values: np.ndarray) -> str:
     return h.hexdigest()
 
 
+def host_info() -> dict:
+    """The GPU box's host CPU (SURVEY.md §8(d): report nproc and the CPU model;
+    the baselines use one core, like the reference fl-cpu)."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"nproc": os.cpu_count(), "cpu_model": model}
+
+
 def cpu_baseline(kind: str, seed: int, sample: int, gpu_bits, gpu_values):
     """Time the oracle (1 core, the reference fl-cpu's algorithm and loops) on
     the first `sample` bytes of the same workload; also compare its output with
@@ -94,6 +109,7 @@ def cpu_baseline(kind: str, seed: int, sample: int, gpu_bits, gpu_values):
         "value": round(sample / (t2 - t0) / 1e9, 4),
         "unit": "GB/s",
         "cores": 1,
+        "host": host_info(),
         "kind": "port",
         "sample": f"{sample} bytes ({kind}, seed {seed}) = the first {sample} bytes of rank 0's "
                   f"workload; oracle/flrl_oracle.c encode {t1 - t0:.2f} s + decode {t2 - t1:.2f} s, "
@@ -221,7 +237,8 @@ def rl_section(n: int, seed: int, steps: int, warmup: int, dev, cpu: bool):
         same = bool(counts.size == R and np.array_equal(d.counts[:R].cpu().numpy(), counts)
                     and np.array_equal(d.values[:R].cpu().numpy(), values))
         res["cpu_baseline"] = {
-            "value": round(n / (t2 - t0) / 1e9, 4), "unit": "GB/s", "cores": 1, "kind": "port",
+            "value": round(n / (t2 - t0) / 1e9, 4), "unit": "GB/s", "cores": 1, "host": host_info(),
+            "kind": "port",
             "sample": f"the full {n}-byte runs32 input; oracle rl encode {t1 - t0:.2f} s + "
                       f"decode {t2 - t1:.2f} s, single-threaded",
             "roundtrip_ok": bool(np.array_equal(back, a)), "gpu_bytes_equal_oracle": same,
