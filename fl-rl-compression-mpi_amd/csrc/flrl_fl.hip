@@ -145,7 +145,8 @@ __device__ __forceinline__ void stage_packed(uint8_t *s, uint32_t off, uint32_t 
 // wave issues no bulk memory operations: vmcnt is per wave and in order, so
 // its status loads would otherwise wait behind them. A/B against the look-back
 // done by data wave 0 (scripts/ab_encode.py): lo4 -11 %, zero -3 %, 16 GiB u8
-// -2 %, 1 GiB u8 equal.
+// -2 %, 1 GiB u8 equal. It also takes the tickets (a data wave would wait for
+// its stores to drain before the atomic returns: 16 GiB u8 -2.9 %).
 // Per-tile timestamp hook for scripts/ubench_fl.hip (no-op in the library).
 #ifndef FLRL_FL_TRACE
 #define FLRL_FL_TRACE(tile, k) ((void)0)
