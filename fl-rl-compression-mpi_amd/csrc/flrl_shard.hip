@@ -13,6 +13,7 @@
 // flrl_fl_compress.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -43,15 +44,15 @@ struct Shard {
 int shard_encode(Shard &s, const uint8_t *data, int ngpus)
 {
     if (hipSetDevice(s.dev) != hipSuccess)
-        return FLRL_E_HIP;
+        return set_error(FLRL_E_HIP, "hipSetDevice(%d) failed", s.dev);
     const size_t in_b = round_up(s.len ? s.len : 1, 16), bits_b = round_up(s.frames + 1, 16);
     const size_t val_b = flrl_fl_values_capacity(s.len);
     const size_t sizes_b = round_up(16 + 16 * (size_t)ngpus, 16);
     s.scr_b = flrl_fl_scratch_bytes(s.len);
     if (hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking) != hipSuccess)
-        return FLRL_E_HIP;
+        return set_error(FLRL_E_HIP, "hipStreamCreate failed on device %d", s.dev);
     if (hipMalloc(&s.base, in_b + bits_b + val_b + sizes_b + s.scr_b) != hipSuccess)
-        return FLRL_E_NOMEM;
+        return set_error(FLRL_E_NOMEM, "Cannot allocate memory (device %d)", s.dev);
     uint8_t *p = static_cast<uint8_t *>(s.base);
     s.d_in = p;
     s.d_bits = p + in_b;
@@ -61,16 +62,16 @@ int shard_encode(Shard &s, const uint8_t *data, int ngpus)
     s.d_scr = p + in_b + bits_b + val_b + sizes_b;
     if (s.len && hipMemcpyAsync(s.d_in, data + s.off, s.len, hipMemcpyHostToDevice, s.stream) !=
                      hipSuccess)
-        return FLRL_E_HIP;
+        return set_error(FLRL_E_HIP, "shard upload failed on device %d", s.dev);
     int rc = flrl_fl_encode_device(s.d_in, s.len, s.d_bits, s.d_vals, s.d_sizes + 1, s.d_scr,
                                    s.scr_b, s.stream);
     if (rc)
         return rc;
     const uint64_t f = s.frames;
     if (hipMemcpyAsync(s.d_sizes, &f, sizeof(f), hipMemcpyHostToDevice, s.stream) != hipSuccess)
-        return FLRL_E_HIP;
-    if (hipStreamSynchronize(s.stream) != hipSuccess)
-        return FLRL_E_HIP;
+        return set_error(FLRL_E_HIP, "frame-count upload failed on device %d", s.dev);
+    if (hipStreamSynchronize(s.stream) != hipSuccess)  // also keeps &f alive for the copy
+        return set_error(FLRL_E_HIP, "stream sync failed on device %d", s.dev);
     return FLRL_OK;
 }
 
@@ -117,14 +118,20 @@ extern "C" int flrl_fl_compress_sharded(const uint8_t *data, size_t size, int ng
     {
         std::vector<std::thread> th;
         for (size_t r = 0; r < P; ++r)
-            th.emplace_back([&, r]() { sh[r].rc = shard_encode(sh[r], data, ngpus); });
+            th.emplace_back([&, r]() {
+                clear_error();
+                sh[r].rc = shard_encode(sh[r], data, ngpus);
+                if (sh[r].rc)  // the last-error string is per thread: keep the worker's
+                    snprintf(sh[r].err, sizeof(sh[r].err), "%s", flrl_last_error());
+            });
         for (auto &t : th)
             t.join();
     }
     for (size_t r = 0; r < P; ++r)
         if (sh[r].rc) {
             cleanup();
-            return set_error(sh[r].rc, "flrl_fl_compress_sharded: shard %zu encode failed", r);
+            return set_error(sh[r].rc, "flrl_fl_compress_sharded: shard %zu encode failed%s%s", r,
+                             sh[r].err[0] ? ": " : "", sh[r].err);
         }
 
     // ---- the one exchange step: AllGather {F_r, V_r} over xGMI -------------

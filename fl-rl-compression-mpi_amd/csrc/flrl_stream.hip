@@ -44,19 +44,31 @@ constexpr size_t kDefaultChunk = 64ull << 20;  // 64 MiB per chunk
 constexpr size_t kHeader = 24;
 constexpr size_t kFrame = FLRL_FRAME_LENGTH;
 
-// First failure of any thread, re-raised on the calling thread.
+// First failure of any thread, re-raised on the calling thread. With a waiter
+// (mutex + condition variable whose predicates test `failed`), set() wakes it:
+// taking the waiters' mutex between the store and the notify means no waiter
+// can have tested the predicate before the store and still be about to sleep.
+// set() must not be called with the waiters' mutex held.
 struct Failure {
     std::mutex m;
     std::atomic<bool> failed{false};
     int code = FLRL_OK;
     std::string msg;
+    std::mutex *wait_m = nullptr;
+    std::condition_variable *wait_cv = nullptr;
     void set(int c, const std::string &s)
     {
-        std::lock_guard<std::mutex> g(m);
-        if (!failed.load()) {
-            code = c;
-            msg = s;
-            failed.store(true);
+        {
+            std::lock_guard<std::mutex> g(m);
+            if (!failed.load()) {
+                code = c;
+                msg = s;
+                failed.store(true);
+            }
+        }
+        if (wait_cv) {
+            { std::lock_guard<std::mutex> g(*wait_m); }
+            wait_cv->notify_all();
         }
     }
 };
@@ -207,6 +219,8 @@ extern "C" int flrl_fl_compress_file(const char *in_path, const char *out_path, 
     Failure fail;
     std::mutex m;
     std::condition_variable cv;
+    fail.wait_m = &m;
+    fail.wait_cv = &cv;
     std::vector<Ready> ready(nchunks);
     const int nw = (int)(W < (int)(nchunks ? nchunks : 1) ? W : (nchunks ? nchunks : 1));
     std::vector<std::atomic<bool>> slot_free((size_t)nw * 2);
@@ -430,8 +444,10 @@ extern "C" int flrl_fl_decompress_file(const char *in_path, const char *out_path
         }
         auto finish = [&](size_t c, int k) -> bool {  // wait, check, write chunk c
             Slot &x = S.slot[k];
-            if (hipStreamSynchronize(x.s) != hipSuccess)
+            if (hipStreamSynchronize(x.s) != hipSuccess) {
+                fail.set(FLRL_E_HIP, "fl decode: stream failed");
                 return false;
+            }
             const int kerr = flrl_scratch_error(x.d_scr, x.s);
             if (kerr) {
                 fail.set(kerr, "fl decode: malformed data (widths or valuesSize)");
@@ -613,6 +629,8 @@ extern "C" int flrl_rl_compress_file(const char *in_path, const char *out_path, 
     Failure fail;
     std::mutex m;
     std::condition_variable cv;
+    fail.wait_m = &m;
+    fail.wait_cv = &cv;
     std::vector<Ready> ready(nchunks);
     const int nw = (int)(W < (int)(nchunks ? nchunks : 1) ? W : (nchunks ? nchunks : 1));
     std::vector<std::atomic<bool>> slot_free((size_t)nw * 2);
@@ -840,8 +858,10 @@ extern "C" int flrl_rl_decompress_file(const char *in_path, const char *out_path
         };
         auto finish = [&](size_t b, int k) -> bool {
             Slot &x = S.slot[k];
-            if (hipStreamSynchronize(x.s) != hipSuccess)
+            if (hipStreamSynchronize(x.s) != hipSuccess) {
+                fail.set(FLRL_E_HIP, "rl decode: stream failed");
                 return false;
+            }
             const int kerr = flrl_scratch_error(x.d_scr, x.s);
             if (kerr) {
                 fail.set(kerr, "rl decode: malformed counts");

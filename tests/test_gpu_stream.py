@@ -138,6 +138,23 @@ def test_cli_streamed_error_removes_output(cli_path, tmp_path):
     assert not out.exists()
 
 
+@pytest.mark.parametrize("method", ["fl", "rl"])
+def test_cli_streamed_read_failure_reported(cli_path, tmp_path, method):
+    """A worker's read failure must wake the in-order writer and surface as an
+    error (it used to leave the writer waiting forever). A directory opens and
+    stats fine but every pread fails (EISDIR)."""
+    src = tmp_path / "dir"
+    src.mkdir()
+    if os.stat(src).st_size == 0:
+        pytest.skip("directory size 0 on this filesystem: no chunk to read")
+    out = tmp_path / "out"
+    env = dict(os.environ, FLRL_CHUNK_BYTES=str(128 * 8), FLRL_WORKERS="2")
+    r = subprocess.run([cli_path, "c", method, str(src), str(out)], env=env, capture_output=True,
+                       text=True, timeout=60)
+    assert r.returncode != 0 and "[ERROR]" in r.stderr, (r.returncode, r.stderr)
+    assert "Cannot read file content" in r.stderr
+
+
 def test_large_file_default_chunks(tmp_path):
     n = (300 << 20) + 4097  # 5 default 64 MiB chunks, ragged tail
     data = oracle.gen("u8", n, 42)
