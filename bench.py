@@ -133,6 +133,20 @@ def workload_ref(n: int, kind: str, world: int) -> str:
     return "custom size"
 
 
+def created_events(rows: int, cols: int, stream) -> list:
+    """rows x cols timing events, each recorded once so its HIP event exists
+    (flrl.time_next_kernel takes the raw handle)."""
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(cols)] for _ in range(rows)]
+    for row in ev:
+        for e in row:
+            e.record(stream)
+    return ev
+
+
+def mean_ms(ev, a: int, b: int) -> float:
+    return float(np.mean([e[a].elapsed_time(e[b]) for e in ev]))
+
+
 def north_star_section(seed: int, steps: int, warmup: int, dev):
     """BASELINE north star: FL encode of 16 GiB uniform-random bytes on 1 GPU,
     target >= 70 % of HBM peak on algorithmic bytes. Encode and
@@ -146,15 +160,17 @@ def north_star_section(seed: int, steps: int, warmup: int, dev):
     for _ in range(max(1, warmup)):
         codec.encode(x)
     v = codec.values_size()
-    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(2)] for _ in range(steps)]
+    ev = created_events(steps, 4, stream)  # call start/end, kernel start/end
     torch.cuda.synchronize()
     for k in range(steps):
         ev[k][0].record(stream)
+        flrl.time_next_kernel(ev[k][2], ev[k][3])
         codec.encode(x)
         ev[k][1].record(stream)
     torch.cuda.synchronize()
     err = codec.error()
-    enc_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in ev]))
+    enc_call_ms = mean_ms(ev, 0, 1)
+    enc_ms = mean_ms(ev, 2, 3)
     f1 = (1 << 30) // 128
     v1 = int(codec.bits[:f1].to(torch.int64).sum().item()) * 16
     h = hashlib.sha256(struct.pack("<QQQ", 1 << 30, f1, v1))
@@ -162,23 +178,29 @@ def north_star_section(seed: int, steps: int, warmup: int, dev):
     h.update(codec.values[:v1].cpu().numpy().tobytes())
     prefix_ok = seed == 42 and h.hexdigest() == GOLDEN_1GIB_U8_SHA
     out = torch.empty_like(x)
-    d0, d1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    (d0, d1, k0, k1), = created_events(1, 4, stream)
     codec.decode(v, out=out)
     d0.record(stream)
+    flrl.time_next_kernel(k0, k1)
     codec.decode(v, out=out)
     d1.record(stream)
     torch.cuda.synchronize()
-    dec_ms = d0.elapsed_time(d1)
+    dec_call_ms = d0.elapsed_time(d1)
+    dec_ms = k0.elapsed_time(k1)
     ok = bool(torch.equal(out, x)) and err == 0 and codec.error() == 0
     alg = n + codec.frames + v
     res = {
         "workload": f"FL encode of {n} u8 bytes (seed {seed}) on 1 GPU (BASELINE north star)",
+        "timing": "kernel time (HIP events around the kernel, flrl_time_next_kernel); call = + scratch memset"
+                  " (decode: + offsets pre-pass)",
         "encode_ms": round(enc_ms, 4),
+        "encode_call_ms": round(enc_call_ms, 4),
         "encode_alg_GBps": round(alg / (enc_ms * 1e-3) / 1e9, 1),
         "encode_input_GBps": round(n / (enc_ms * 1e-3) / 1e9, 1),
         "frac": round(alg / (enc_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
         "target_frac": 0.70,
         "decode_ms": round(dec_ms, 4),
+        "decode_call_ms": round(dec_call_ms, 4),
         "decode_alg_GBps": round(alg / (dec_ms * 1e-3) / 1e9, 1),
         "roundtrip": ok,
         "prefix_1GiB_matches_reference_fl_cpu": prefix_ok,
@@ -202,28 +224,32 @@ def rl_section(n: int, seed: int, steps: int, warmup: int, dev, cpu: bool):
     for _ in range(warmup):
         d.encode(x)
         d.decode(R)
-    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(steps)]
+    ev = created_events(steps, 7, stream)  # calls: 0-1-2; kernels: 3-4 encode, 5-6 decode
     torch.cuda.synchronize()
     for k in range(steps):
         ev[k][0].record(stream)
+        flrl.time_next_kernel(ev[k][3], ev[k][4])
         d.encode(x)
         ev[k][1].record(stream)
+        flrl.time_next_kernel(ev[k][5], ev[k][6])
         d.decode(R)
         ev[k][2].record(stream)
     torch.cuda.synchronize()
     assert d.error() == 0
-    enc_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in ev]))
-    dec_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in ev]))
+    enc_ms, dec_ms = mean_ms(ev, 0, 1), mean_ms(ev, 1, 2)  # whole calls
+    enc_k, dec_k = mean_ms(ev, 3, 4), mean_ms(ev, 5, 6)      # kernels alone
     alg = n + 2 * R  # RL encode N+2R, decode 2R+N
     res = {
         "workload": f"RL encode+decode of {n} bytes runs32 (seed {seed}), BASELINE configs[2]",
         "runs": R,
         "value": round(n / ((enc_ms + dec_ms) * 1e-3) / 1e9, 2),
         "unit": "GB/s (input bytes, encode+decode)",
-        "rl_encode": {"ms": round(enc_ms, 4), "alg_GBps": round(alg / (enc_ms * 1e-3) / 1e9, 1),
-                      "frac": round(alg / (enc_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
-        "rl_decode": {"ms": round(dec_ms, 4), "alg_GBps": round(alg / (dec_ms * 1e-3) / 1e9, 1),
-                      "frac": round(alg / (dec_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
+        "rl_encode": {"ms": round(enc_k, 4), "call_ms": round(enc_ms, 4),
+                      "alg_GBps": round(alg / (enc_k * 1e-3) / 1e9, 1),
+                      "frac": round(alg / (enc_k * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
+        "rl_decode": {"ms": round(dec_k, 4), "call_ms": round(dec_ms, 4),
+                      "alg_GBps": round(alg / (dec_k * 1e-3) / 1e9, 1),
+                      "frac": round(alg / (dec_k * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
         "roundtrip": ok,
     }
     if cpu:
@@ -295,6 +321,7 @@ def main():
     def step(e=None):
         if e is not None:
             e[0].record(stream)
+            flrl.time_next_kernel(e[4], e[5])
         codec.encode(x)
         if e is not None:
             e[1].record(stream)
@@ -310,6 +337,8 @@ def main():
                 e[2].record(stream)
         elif e is not None:
             e[2].record(stream)
+        if e is not None:
+            flrl.time_next_kernel(e[6], e[7])
         codec.decode(v, out=out)
         if e is not None:
             e[3].record(stream)
@@ -341,7 +370,8 @@ def main():
     copy_gbs = 2 * n / (copy_ms * 1e-3) / 1e9
 
     # ---- timed region: K steps ----
-    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(args.steps)]
+    # 0-3: step phases (encode call, size-scan, decode call); 4-7: encode / decode kernels alone
+    ev = created_events(args.steps, 8, stream)
     if scan:
         dist.barrier()
     torch.cuda.synchronize()
@@ -356,12 +386,10 @@ def main():
         t = torch.tensor([wall], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         wall = float(t.item())
-    enc_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in ev]))
-    scan_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in ev]))  # side stream: concurrent with decode
-    if scan and args.scan == "side":
-        dec_ms = float(np.mean([e[1].elapsed_time(e[3]) for e in ev]))
-    else:
-        dec_ms = float(np.mean([e[2].elapsed_time(e[3]) for e in ev]))
+    enc_call_ms = mean_ms(ev, 0, 1)  # + scratch memset
+    scan_ms = mean_ms(ev, 1, 2)  # side stream: concurrent with decode
+    dec_call_ms = mean_ms(ev, 1, 3) if scan and args.scan == "side" else mean_ms(ev, 2, 3)  # + memset, offsets
+    enc_ms, dec_ms = mean_ms(ev, 4, 5), mean_ms(ev, 6, 7)  # the kernels alone
     assert codec.error() == 0
 
     ms_per_step = wall * 1e3 / args.steps
@@ -431,9 +459,14 @@ def main():
                 "algorithmic_bytes_per_launch": alg,
             },
             "kernels": {
-                "fl_encode": {"ms": round(enc_ms, 4), "alg_GBps": round(enc_gbs, 1),
+                "timing": "ms = the kernel alone (HIP events recorded by flrl_time_next_kernel on the "
+                          "launch stream); call_ms = the whole device call (+ scratch memset; decode: + "
+                          "offsets pre-pass)",
+                "fl_encode": {"ms": round(enc_ms, 4), "call_ms": round(enc_call_ms, 4),
+                              "alg_GBps": round(enc_gbs, 1),
                               "input_GBps": round(n / (enc_ms * 1e-3) / 1e9, 1)},
-                "fl_decode": {"ms": round(dec_ms, 4), "alg_GBps": round(dec_gbs, 1),
+                "fl_decode": {"ms": round(dec_ms, 4), "call_ms": round(dec_call_ms, 4),
+                              "alg_GBps": round(dec_gbs, 1),
                               "output_GBps": round(n / (dec_ms * 1e-3) / 1e9, 1)},
                 "size_scan": {"ms": round(scan_ms, 4), "stream": args.scan if scan else None},
                 "device_copy_ceiling": {"ms": round(copy_ms, 4), "GBps": round(copy_gbs, 1),

@@ -24,6 +24,22 @@ int set_error(int code, const char *fmt, ...)
 
 void clear_error() { g_err[0] = 0; }
 
+// Pending kernel-timing events of this thread (flrl_time_next_kernel).
+static thread_local hipEvent_t g_ev_start = nullptr, g_ev_stop = nullptr;
+
+void kernel_timing_begin(hipStream_t s)
+{
+    if (g_ev_start)
+        (void)hipEventRecord(g_ev_start, s);
+}
+
+void kernel_timing_end(hipStream_t s)
+{
+    if (g_ev_stop)
+        (void)hipEventRecord(g_ev_stop, s);
+    g_ev_start = g_ev_stop = nullptr;
+}
+
 // splitmix64 draw number w+1 from `seed` (counter form of SURVEY.md §8(d)).
 __device__ __forceinline__ uint64_t splitmix_at(uint64_t seed, uint64_t w)
 {
@@ -55,6 +71,15 @@ using namespace flrl;
 extern "C" const char *flrl_last_error(void) { return g_err; }
 
 extern "C" const char *flrl_version(void) { return "flrl 0.1.0 (gfx950)"; }
+
+extern "C" int flrl_time_next_kernel(void *start_event, void *stop_event)
+{
+    if ((start_event == nullptr) != (stop_event == nullptr))
+        return set_error(FLRL_E_ARG, "flrl_time_next_kernel: pass both events or neither");
+    g_ev_start = static_cast<hipEvent_t>(start_event);
+    g_ev_stop = static_cast<hipEvent_t>(stop_event);
+    return FLRL_OK;
+}
 
 extern "C" int flrl_device_count(void)
 {

@@ -657,9 +657,11 @@ extern "C" int flrl_fl_encode_device(const uint8_t *d_in, size_t n, uint8_t *d_b
     uint64_t *status = reinterpret_cast<uint64_t *>(ctrl + 1);
     const size_t resident = (size_t)cu_count();
     const uint32_t grid = (uint32_t)(L.enc_tiles < resident ? L.enc_tiles : resident);
+    kernel_timing_begin(s);
     hipLaunchKernelGGL((fl_encode_kernel<kEncThreads, kEncItems>), dim3(grid), dim3(kEncThreads + kWave),
                        0, s, d_in, (uint64_t)n, (uint64_t)div_up(n, kFrame), (uint32_t)L.enc_tiles,
                        d_bits, d_values, d_values_size, ctrl, status);
+    kernel_timing_end(s);
     FLRL_HIP(hipGetLastError());
     return FLRL_OK;
 }
@@ -699,10 +701,12 @@ extern "C" int flrl_fl_decode_device(const uint8_t *d_bits, size_t bits_size,
                        (uint32_t)L.dec_tiles, (uint32_t)L.off_blocks, (uint32_t)L.off_iters, ctrl, status);
     FLRL_HIP(hipGetLastError());
     const size_t dgrid = (size_t)kDecPerCU * (size_t)cu_count();
+    kernel_timing_begin(s);
     hipLaunchKernelGGL(fl_decode_kernel<kDecItems>,
                        dim3((uint32_t)(L.dec_tiles < dgrid ? L.dec_tiles : dgrid)), dim3(kDecThreads), 0,
                        s, d_bits, (uint64_t)bits_size, d_values, (uint64_t)values_size, d_out,
                        (uint64_t)n, tile_base, (uint32_t)L.dec_tiles, ctrl, (uint32_t)L.off_blocks);
+    kernel_timing_end(s);
     FLRL_HIP(hipGetLastError());
     return FLRL_OK;
 }

@@ -17,6 +17,11 @@ namespace flrl {
 int set_error(int code, const char *fmt, ...);
 void clear_error();
 
+// flrl_time_next_kernel: record this thread's pending start/stop events on `s`
+// tightly around a device call's main kernel (no-ops when none are pending).
+void kernel_timing_begin(hipStream_t s);
+void kernel_timing_end(hipStream_t s);
+
 inline size_t div_up(size_t a, size_t b) { return (a + b - 1) / b; }
 inline size_t round_up(size_t a, size_t b) { return div_up(a, b) * b; }
 

@@ -1148,8 +1148,10 @@ extern "C" int flrl_rl_encode_device(const uint8_t *d_in, size_t n, uint8_t *d_c
         return set_error(FLRL_E_ARG, "flrl_rl_encode_device: input too large");
     Ctrl *ctrl = static_cast<Ctrl *>(d_scratch);
     uint64_t *status = reinterpret_cast<uint64_t *>(ctrl + 1);
+    kernel_timing_begin(s);
     hipLaunchKernelGGL((rl_encode_kernel<kRlThreads, kRlLaneBytes, kRlSub>), dim3((uint32_t)L.tiles), dim3(kRlThreads),
                        FLRL_RL_DYN_LDS, s, d_in, (uint64_t)n, (uint32_t)L.tiles, d_counts, d_values, d_runs, ctrl, status);
+    kernel_timing_end(s);
     FLRL_HIP(hipGetLastError());
     return FLRL_OK;
 }
@@ -1192,8 +1194,10 @@ extern "C" int flrl_rl_decode_device(const uint8_t *d_counts, const uint8_t *d_v
                        (uint32_t)L.blocks, (uint32_t)L.iters, ctrl, status);
     FLRL_HIP(hipGetLastError());
     const size_t rgrid = (size_t)kRdPerCU * (size_t)cu_count();
+    kernel_timing_begin(s);
     hipLaunchKernelGGL(rl_decode_kernel, dim3((uint32_t)(L.tiles < rgrid ? L.tiles : rgrid)), dim3(kRdThreads), 0,
                        s, d_counts, d_values, (uint64_t)runs, d_out, (uint64_t)n, tile_base, (uint64_t)L.tiles);
+    kernel_timing_end(s);
     FLRL_HIP(hipGetLastError());
     return FLRL_OK;
 }

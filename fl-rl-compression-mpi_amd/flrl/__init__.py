@@ -106,6 +106,7 @@ _sig("flrl_fl_values_capacity", _sz, _sz)
 _sig("flrl_fl_encode_device", ctypes.c_int, _vp, _sz, _vp, _vp, _vp, _vp, _sz, _vp)
 _sig("flrl_fl_decode_device", ctypes.c_int, _vp, _sz, _vp, _sz, _vp, _sz, _vp, _sz, _vp)
 _sig("flrl_scratch_error", ctypes.c_int, _vp, _vp)
+_sig("flrl_time_next_kernel", ctypes.c_int, _vp, _vp)
 _sig("flrl_rl_compress", ctypes.c_int, _vp, _sz, ctypes.POINTER(_RLBuf))
 _sig("flrl_rl_decompress", ctypes.c_int, _sz, _vp, _vp, _sz,
      ctypes.POINTER(_u8p), ctypes.POINTER(_sz))
@@ -300,6 +301,20 @@ def gen_host(kind, n: int, seed: int, word_offset: int = 0) -> np.ndarray:
     return out
 
 
+def time_next_kernel(start=None, stop=None) -> None:
+    """Record two events (torch.cuda.Event or raw hipEvent_t ints; already
+    created, i.e. recorded once) around the main kernel of this thread's next
+    device call; see flrl_time_next_kernel in include/flrl.h."""
+    def handle(e):
+        if e is None:
+            return None
+        h = e.cuda_event if hasattr(e, "cuda_event") else int(e)
+        if not h:
+            raise ValueError("event not created yet: record it once first")
+        return h
+    _check(_lib.flrl_time_next_kernel(handle(start), handle(stop)))
+
+
 def scratch_error(d_scratch: int, stream: int = 0) -> int:
     rc = _lib.flrl_scratch_error(d_scratch, stream or None)
     return int(rc)
@@ -323,7 +338,8 @@ def parse_fl_file(blob: bytes) -> FLCompressed:
 def rl_file_bytes(input_size: int, counts, values) -> bytes:
     """RL container (build-defined): u64 inputSize | u64 runs | counts | values."""
     c, v = _as_u8(counts), _as_u8(values)
-    assert c.size == v.size
+    if c.size != v.size:
+        raise ValueError(f"RL counts ({c.size}) and values ({v.size}) differ in length")
     return struct.pack("<QQ", input_size, c.size) + c.tobytes() + v.tobytes()
 
 

@@ -142,6 +142,15 @@ int flrl_fl_decode_device(const uint8_t *d_bits, size_t bits_size, const uint8_t
  * 0 = ok, else an FLRL_E_* code. */
 int flrl_scratch_error(const void *d_scratch, void *stream);
 
+/* Measurement hook (no reference counterpart): the next flrl_*_device call of
+ * this thread that launches its kernels records `start_event` on its stream
+ * immediately before its main kernel (fl_encode, fl_decode, rl_encode,
+ * rl_decode) and `stop_event` immediately after it, so the caller's
+ * hipEventElapsedTime covers that kernel alone (not the scratch memset or the
+ * decode offsets pre-pass). Events are hipEvent_t created by the caller; both
+ * NULL cancels a pending pair. */
+int flrl_time_next_kernel(void *start_event, void *stop_event);
+
 /* ---- RL, host buffers (synchronous) --------------------------------------- */
 int flrl_rl_compress(const uint8_t *data, size_t size, flrl_rl_buf *out);
 int flrl_rl_decompress(size_t output_size, const uint8_t *counts, const uint8_t *values,

@@ -74,3 +74,13 @@ def test_file_codec_needs_device(tmp_path):
         with pytest.raises(flrl.FLRLError) as e:
             fn(str(src), str(tmp_path / "out"), 1, 0)
         assert e.value.code == flrl.E_NODEV
+
+
+def test_time_next_kernel_arguments():
+    """The measurement hook takes both events or neither (no GPU work)."""
+    f = flrl.lib_handle().flrl_time_next_kernel
+    assert f(ctypes.c_void_p(16), None) == flrl.E_ARG
+    assert f(None, ctypes.c_void_p(16)) == flrl.E_ARG
+    assert f(None, None) == flrl.E_OK
+    with pytest.raises(ValueError):
+        flrl.time_next_kernel(0, 0)  # a not-yet-created event handle

@@ -320,3 +320,49 @@ def test_cli_rl_gpu(bmp_bytes, cli_path, tmp_path):
     subprocess.run([cli_path, "d", "rl", str(tmp_path / "o.rl"), str(tmp_path / "b")], check=True,
                    capture_output=True)
     assert (tmp_path / "b").read_bytes() == bmp_bytes
+
+
+@pytest.mark.gpu
+def test_time_next_kernel_brackets_the_kernel():
+    """flrl_time_next_kernel: the kernel window lies inside the call window
+    (the call adds the scratch memset; decode also the offsets pre-pass), the
+    pair is consumed by one call, and results are unaffected."""
+    from flrl.device import FLDevice, RLDevice, gen
+    n = (32 << 20) + 77
+    x = gen("u8", n, 5)
+    s = torch.cuda.current_stream()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+    for e in ev:
+        e.record(s)
+    d = FLDevice(n)
+    for call in (lambda: d.encode(x), lambda: d.decode(d.values_size())):
+        call()
+        torch.cuda.synchronize()
+        ev[0].record(s)
+        flrl.time_next_kernel(ev[2], ev[3])
+        call()
+        ev[1].record(s)
+        torch.cuda.synchronize()
+        whole, kern = ev[0].elapsed_time(ev[1]), ev[2].elapsed_time(ev[3])
+        assert 0 < kern <= whole, (kern, whole)
+        assert ev[0].elapsed_time(ev[2]) >= 0 and ev[3].elapsed_time(ev[1]) >= 0
+    assert torch.equal(d.out[:n], x[:n]) and d.error() == 0
+    # consumed: a further call leaves the events where they were
+    t = ev[2].elapsed_time(ev[3])
+    d.encode(x)
+    torch.cuda.synchronize()
+    assert ev[2].elapsed_time(ev[3]) == t
+    r = RLDevice(n)
+    ev[0].record(s)
+    flrl.time_next_kernel(ev[2], ev[3])
+    r.encode(x)
+    ev[1].record(s)
+    torch.cuda.synchronize()
+    assert 0 < ev[2].elapsed_time(ev[3]) <= ev[0].elapsed_time(ev[1])
+    flrl.time_next_kernel(ev[2], ev[3])
+    flrl.time_next_kernel(None, None)  # cancel
+    ev[0].record(s)
+    r.decode(r.runs())
+    ev[1].record(s)
+    torch.cuda.synchronize()
+    assert torch.equal(r.out[:n], x[:n]) and r.error() == 0
