@@ -53,7 +53,8 @@ def parse():
     p.add_argument("--seed", type=int, default=42)
     p.add_argument("--cpu-sample", type=int, default=-1,
                    help="bytes of the workload the CPU oracle times (default: min(bytes, 1 GiB)); 0 = skip")
-    p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"))
+    p.add_argument("--traffic-json", default=None,
+                   help="PMC summary (scripts/summarize_profile.py); default profiles/traffic_<kind>_<bytes>.json")
     p.add_argument("--no-north-star", action="store_true",
                    help="skip the 16 GiB u8 FL encode (BASELINE north-star target) at N=1")
     p.add_argument("--no-rl", action="store_true",
@@ -133,6 +134,20 @@ def workload_ref(n: int, kind: str, world: int) -> str:
     return "custom size"
 
 
+def pmc_traffic(kind: str, n: int, kernel: str, path: str | None = None):
+    """HBM bytes per launch of `kernel` from the committed PMC summary of this
+    exact workload (scripts/profile.sh + summarize_profile.py), else None."""
+    path = path or os.path.join(ROOT, "profiles", f"traffic_{kind}_{n}.json")
+    try:
+        with open(path) as f:
+            tj = json.load(f)
+        if tj.get("bytes") == n and tj.get("kind") == kind:
+            return tj["kernels"].get(kernel, {}).get("hbm_bytes_per_launch")
+    except (OSError, ValueError, KeyError, AttributeError):
+        pass
+    return None
+
+
 def created_events(rows: int, cols: int, stream) -> list:
     """rows x cols timing events, each recorded once so its HIP event exists
     (flrl.time_next_kernel takes the raw handle)."""
@@ -199,6 +214,8 @@ def north_star_section(seed: int, steps: int, warmup: int, dev):
         "encode_input_GBps": round(n / (enc_ms * 1e-3) / 1e9, 1),
         "frac": round(alg / (enc_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
         "target_frac": 0.70,
+        "algorithmic_bytes_per_launch": alg,
+        "traffic": pmc_traffic("u8", n, "fl_encode"),
         "decode_ms": round(dec_ms, 4),
         "decode_call_ms": round(dec_call_ms, 4),
         "decode_alg_GBps": round(alg / (dec_ms * 1e-3) / 1e9, 1),
@@ -401,14 +418,7 @@ def main():
     dec_gbs = alg / (dec_ms * 1e-3) / 1e9
     dominant = "fl_encode" if enc_ms >= dec_ms else "fl_decode"
     achieved = enc_gbs if dominant == "fl_encode" else dec_gbs
-    traffic = None
-    try:
-        with open(args.traffic_json) as f:
-            tj = json.load(f)
-        if tj.get("bytes") == n and tj.get("kind") == args.kind:
-            traffic = tj["kernels"].get(dominant, {}).get("hbm_bytes_per_launch")
-    except (OSError, ValueError, KeyError):
-        traffic = None
+    traffic = pmc_traffic(args.kind, n, dominant, args.traffic_json)
 
     if scan:
         for key in ("roundtrip", "size_scan_ok"):

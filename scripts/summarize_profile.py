@@ -4,7 +4,7 @@
 Reads gpurun_out/prof/<tag>/{trace,fetch,write}/*.csv and writes
   profiles/<tag>_kernel_stats.csv   rocprofv3 --stats summary (verbatim)
   profiles/<tag>_summary.json       per-kernel avg duration, HBM bytes/launch
-  profiles/traffic_latest.json      read by bench.py for roofline.traffic
+  profiles/traffic_<kind>_<bytes>.json  read by bench.py for roofline.traffic of that workload
 HBM bytes follow MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE are KiB;
 on gfx950 FETCH_SIZE reports half the bytes of a wide (16 B/lane) coalesced
 streaming read, so it is doubled; WRITE_SIZE is exact for 16-B stores.
@@ -76,7 +76,7 @@ def main():
                "kernels": kernels}
     with open(os.path.join(dst, f"{a.tag}_summary.json"), "w") as f:
         json.dump(summary, f, indent=1)
-    with open(os.path.join(dst, "traffic_latest.json"), "w") as f:
+    with open(os.path.join(dst, f"traffic_{a.kind}_{a.bytes}.json"), "w") as f:
         json.dump(summary, f, indent=1)
     print(json.dumps(summary, indent=1))
 
