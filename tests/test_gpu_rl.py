@@ -190,3 +190,43 @@ def test_decode_all_starts_in_chunk():
                         np.repeat((np.arange(40_000) % 2 + 5).astype(np.uint8), 2),
                         np.repeat((np.arange(40_000) % 3 + 9).astype(np.uint8), 3)])
     check(a)
+
+
+def test_device_more_than_2_32_runs():
+    """64-bit run indices: ~4.27 GiB of random bytes has R > 2^32 runs (all
+    shorter than 255). Device round trip; R against an independent torch count
+    of run starts; and the records of three windows that start at run starts
+    (the head, around record 2^32, the tail) bit-exact against the oracle."""
+    from flrl.device import RLDevice, gen
+    n = (1 << 32) + (1 << 28) + 12345
+    x = gen("u8", n, 77)
+    d = RLDevice(n)
+    d.encode(x)
+    R = d.runs()
+    assert d.error() == 0
+    changes = (x[1:n] != x[: n - 1])
+    expect = int(changes.sum().item()) + 1
+    assert R == expect and R > (1 << 32), (R, expect)
+
+    def window(i0: int, length: int):
+        """records of x[i0 : i0+length] (i0 moved to the next run start, the end
+        moved back to a run end) and the index of its first record"""
+        i0 = max(i0, 1)
+        while bool(x[i0] == x[i0 - 1]):
+            i0 += 1
+        i1 = min(i0 + length, n)
+        while i1 < n and bool(x[i1] == x[i1 - 1]):
+            i1 -= 1
+        k0 = int(changes[: i0 - 1].sum().item()) + 1  # runs starting before i0
+        return k0, x[i0:i1].cpu().numpy()
+
+    for k0, a in [(0, x[: 1 << 20].cpu().numpy())] + [window(i, 1 << 20) for i in
+                                                        (int((1 << 32) * 256 / 255) - (1 << 19), n - (1 << 20))]:
+        c, v = oracle.rl_compress(a)
+        assert k0 + c.size <= R
+        assert np.array_equal(d.counts[k0:k0 + c.size].cpu().numpy(), c), k0
+        assert np.array_equal(d.values[k0:k0 + c.size].cpu().numpy(), v), k0
+    del changes
+    out = d.decode(R)
+    assert d.error() == 0
+    assert torch.equal(out[:n], x[:n])
