@@ -40,6 +40,39 @@ void kernel_timing_end(hipStream_t s)
     g_ev_start = g_ev_stop = nullptr;
 }
 
+// Scratch resets. A kernel rather than hipMemsetAsync: captured into a HIP
+// graph (torch.cuda.graph around encode/decode), hipMemsetAsync resets did not
+// take effect on re-launch here (the second replay of an encode + decode step
+// saw the previous launch's ticket: scripts/graph_probe.py), while a kernel
+// node is stream-ordered like the kernels around it.
+__global__ __launch_bounds__(kThreads) void zero_kernel(uint8_t *p, uint64_t bytes)
+{
+    const uint64_t stride = (uint64_t)gridDim.x * kThreads;
+    const uint64_t i = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
+    if ((reinterpret_cast<uintptr_t>(p) & 15u) == 0) {
+        for (uint64_t c = i; c * 16 < bytes; c += stride) {
+            if (c * 16 + 16 <= bytes)
+                *reinterpret_cast<u32x4 *>(p + c * 16) = u32x4{0u, 0u, 0u, 0u};
+            else
+                for (uint64_t b = c * 16; b < bytes; ++b)
+                    p[b] = 0;
+        }
+    } else {
+        for (uint64_t b = i; b < bytes; b += stride)
+            p[b] = 0;
+    }
+}
+
+hipError_t zero_async(void *p, size_t bytes, hipStream_t s)
+{
+    if (bytes == 0)
+        return hipSuccess;
+    const size_t blocks = div_up(div_up(bytes, 16), (size_t)kThreads);
+    hipLaunchKernelGGL(zero_kernel, dim3((uint32_t)(blocks < 1024 ? blocks : 1024)), dim3(kThreads), 0, s,
+                       static_cast<uint8_t *>(p), (uint64_t)bytes);
+    return hipGetLastError();
+}
+
 // splitmix64 draw number w+1 from `seed` (counter form of SURVEY.md §8(d)).
 __device__ __forceinline__ uint64_t splitmix_at(uint64_t seed, uint64_t w)
 {

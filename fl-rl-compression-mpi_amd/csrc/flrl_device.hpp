@@ -6,7 +6,7 @@
 // status word is ONE naturally aligned 8-byte granule that carries its own flag
 // and payload, stored and loaded with agent-scope relaxed atomics (sc1, L1
 // bypass), so no release/acquire fence is needed. Status words are zeroed by a
-// hipMemsetAsync before every launch (Guideline 16, "Re-initialise every call").
+// zero-fill kernel before every launch (Guideline 16, "Re-initialise every call").
 // Tiles are numbered by an atomic ticket in launch order, so the look-back only
 // ever waits on tiles that already hold a ticket (forward progress does not
 // depend on dispatch order); every spin is bounded and reports FLRL_E_TIMEOUT.

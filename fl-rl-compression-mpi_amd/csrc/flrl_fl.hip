@@ -180,6 +180,8 @@ __global__ __launch_bounds__(T + kWave, 1) void fl_encode_kernel(
         s_next[0] = atomicAdd(&ctrl->ticket, 1u);
     __syncthreads();
     uint32_t tile = s_next[0];
+    // not an error: a workgroup dispatched late (the GPU shared with other
+    // work) can find every tile taken by the others
     if (tile >= ntiles)
         return;
     uint32_t slot = 1;
@@ -642,8 +644,8 @@ extern "C" int flrl_fl_encode_device(const uint8_t *d_in, size_t n, uint8_t *d_b
     if (!aligned16(d_scratch))
         return set_error(FLRL_E_ARG, "flrl_fl_encode_device: scratch not 16-byte aligned");
     if (n == 0) {
-        FLRL_HIP(hipMemsetAsync(d_scratch, 0, sizeof(Ctrl), s));
-        FLRL_HIP(hipMemsetAsync(d_values_size, 0, sizeof(uint64_t), s));
+        FLRL_HIP(zero_async(d_scratch, sizeof(Ctrl), s));
+        FLRL_HIP(zero_async(d_values_size, sizeof(uint64_t), s));
         return FLRL_OK;
     }
     if (!d_in || !d_bits || !d_values)
@@ -652,7 +654,7 @@ extern "C" int flrl_fl_encode_device(const uint8_t *d_in, size_t n, uint8_t *d_b
         return set_error(FLRL_E_ARG, "flrl_fl_encode_device: buffers must be 16-byte aligned");
     if (L.enc_tiles > 0xFFFFFFFFull)
         return set_error(FLRL_E_ARG, "flrl_fl_encode_device: input too large");
-    FLRL_HIP(hipMemsetAsync(d_scratch, 0, L.enc_zero, s));
+    FLRL_HIP(zero_async(d_scratch, L.enc_zero, s));
     Ctrl *ctrl = static_cast<Ctrl *>(d_scratch);
     uint64_t *status = reinterpret_cast<uint64_t *>(ctrl + 1);
     const size_t resident = (size_t)cu_count();
@@ -680,7 +682,7 @@ extern "C" int flrl_fl_decode_device(const uint8_t *d_bits, size_t bits_size,
     if (!aligned16(d_scratch))
         return set_error(FLRL_E_ARG, "flrl_fl_decode_device: scratch not 16-byte aligned");
     if (n == 0) {
-        FLRL_HIP(hipMemsetAsync(d_scratch, 0, sizeof(Ctrl), s));
+        FLRL_HIP(zero_async(d_scratch, sizeof(Ctrl), s));
         return FLRL_OK;
     }
     if (bits_size != div_up(n, kFrame))
@@ -691,7 +693,7 @@ extern "C" int flrl_fl_decode_device(const uint8_t *d_bits, size_t bits_size,
         return set_error(FLRL_E_ARG, "flrl_fl_decode_device: buffers must be 16-byte aligned");
     if (L.dec_tiles > 0x7FFFFFFFull)
         return set_error(FLRL_E_ARG, "flrl_fl_decode_device: output too large");
-    FLRL_HIP(hipMemsetAsync(d_scratch, 0, L.dec_zero, s));
+    FLRL_HIP(zero_async(d_scratch, L.dec_zero, s));
     Ctrl *ctrl = static_cast<Ctrl *>(d_scratch);
     uint64_t *status = reinterpret_cast<uint64_t *>(ctrl + 1);
     uint64_t *tile_base =

@@ -19,6 +19,9 @@ void clear_error();
 
 // flrl_time_next_kernel: record this thread's pending start/stop events on `s`
 // tightly around a device call's main kernel (no-ops when none are pending).
+// Zero `bytes` at device pointer p on stream s (a kernel, also inside graphs).
+hipError_t zero_async(void *p, size_t bytes, hipStream_t s);
+
 void kernel_timing_begin(hipStream_t s);
 void kernel_timing_end(hipStream_t s);
 

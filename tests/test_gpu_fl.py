@@ -366,3 +366,48 @@ def test_time_next_kernel_brackets_the_kernel():
     ev[1].record(s)
     torch.cuda.synchronize()
     assert torch.equal(r.out[:n], x[:n]) and r.error() == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [1000003, (64 << 20) + 77])
+def test_graph_capture_replays(n):
+    """Device calls captured into a HIP graph (torch.cuda.graph) re-initialise
+    their scratch on every replay: FL and RL encode + decode replayed with every
+    output cleared in between stay bit-exact. (With hipMemsetAsync resets the
+    second replay saw the first one's ticket and the encode did nothing.)"""
+    from flrl.device import FLDevice, RLDevice, gen
+    x = gen("lo4", n, 3)
+    d, r = FLDevice(n), RLDevice(n)
+    d.encode(x)
+    v = d.values_size()
+    r.encode(x)
+    R = r.runs()
+    bits0, vals0 = d.bits[: d.frames].clone(), d.values[:v].clone()
+    c0, rv0 = r.counts[:R].clone(), r.values[:R].clone()
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        d.encode(x)
+        d.decode(v)
+        r.encode(x)
+        r.decode(R)
+    torch.cuda.current_stream().wait_stream(side)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        d.encode(x)
+        d.decode(v)
+        r.encode(x)
+        r.decode(R)
+    for i in range(4):
+        for t in (d.out, d.bits, d.values, r.out, r.counts, r.values):
+            t.zero_()
+        d.sizes[1] = 0
+        r.runs_t.zero_()
+        g.replay()
+        torch.cuda.synchronize()
+        assert d.error() == 0 and r.error() == 0, i
+        assert d.values_size() == v and r.runs() == R, i
+        assert torch.equal(d.bits[: d.frames], bits0) and torch.equal(d.values[:v], vals0), i
+        assert torch.equal(r.counts[:R], c0) and torch.equal(r.values[:R], rv0), i
+        assert torch.equal(d.out[:n], x[:n]) and torch.equal(r.out[:n], x[:n]), i
