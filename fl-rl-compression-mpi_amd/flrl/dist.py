@@ -27,19 +27,32 @@ def shard_range(n: int, rank: int, world: int) -> tuple[int, int]:
     return start, length
 
 
+_SCAN_BUFS: dict = {}
+
+
+def _scan_buf(world: int, device) -> torch.Tensor:
+    """int64[(world + 1) * 2] whose first row stays [0, 0]: the all-gather fills
+    rows 1..world, so ONE cumsum yields every rank's exclusive offsets (rows
+    0..world-1) and the totals (row world)."""
+    key = (world, str(device))
+    buf = _SCAN_BUFS.get(key)
+    if buf is None:
+        buf = torch.zeros((world + 1) * 2, dtype=torch.int64, device=device)
+        _SCAN_BUFS[key] = buf
+    return buf
+
+
 def size_scan(sizes: torch.Tensor, group=None) -> tuple[torch.Tensor, torch.Tensor]:
     """All-gather each rank's int64 [F_r, V_r] and exclusive-scan them.
 
     `sizes` stays on its device (no host sync for a GPU tensor). Returns
     (offsets of this rank [F_off, V_off], totals [F, V]) as int64 tensors on
-    the same device.
+    the same device. Device work: the all-gather and one cumsum kernel.
     """
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     sizes = sizes.reshape(2).to(torch.int64)
-    flat = torch.empty(world * 2, dtype=torch.int64, device=sizes.device)
-    dist.all_gather_into_tensor(flat, sizes, group=group)  # one buffer: no per-rank list + stack
-    allsz = flat.view(world, 2)
-    incl = torch.cumsum(allsz, dim=0)
-    excl = incl - allsz
-    return excl[rank], incl[-1]
+    buf = _scan_buf(world, sizes.device)
+    dist.all_gather_into_tensor(buf[2:], sizes, group=group)  # one buffer: no per-rank list + stack
+    scan = torch.cumsum(buf.view(world + 1, 2), dim=0)
+    return scan[rank], scan[world]
