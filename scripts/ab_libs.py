@@ -61,8 +61,14 @@ def main():
     else:
         x = torch.from_numpy(flrl.gen_host(kind, n, 42)).cuda()
     s = torch.cuda.current_stream().cuda_stream
+    def roomy(d):
+        """scratch with room for builds whose scratch layout is larger"""
+        d.scratch_bytes = 2 * d.scratch_bytes + (1 << 20)
+        d.scratch = torch.empty(d.scratch_bytes, dtype=torch.uint8, device="cuda")
+
     if a.op.startswith("fl"):
         d = FLDevice(n, "cuda")
+        roomy(d)
         d.encode(x)
         V = d.values_size()
 
@@ -81,6 +87,7 @@ def main():
         alg = n + d.frames + V
     else:
         d = RLDevice(n, "cuda")
+        roomy(d)
         d.encode(x)
         R = d.runs()
 
