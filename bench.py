@@ -252,7 +252,8 @@ def rl_section(n: int, seed: int, steps: int, warmup: int, dev, cpu: bool):
         d.decode(R)
         ev[k][2].record(stream)
     torch.cuda.synchronize()
-    assert d.error() == 0
+    if d.error():
+        raise SystemExit(f"RL device error {d.error()} during the timed steps")
     enc_ms, dec_ms = mean_ms(ev, 0, 1), mean_ms(ev, 1, 2)  # whole calls
     enc_k, dec_k = mean_ms(ev, 3, 4), mean_ms(ev, 5, 6)      # kernels alone
     alg = n + 2 * R  # RL encode N+2R, decode 2R+N
@@ -304,7 +305,8 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     n = args.bytes
-    assert n % 128 == 0, "per-GPU bytes must be frame-aligned for weak scaling"
+    if n % 128:
+        raise SystemExit("--bytes must be a multiple of 128 (frame-aligned shards for weak scaling)")
 
     x = gen(args.kind, n, args.seed, word_offset=rank * n // 8, device=dev)
     codec = FLDevice(n, dev)
@@ -414,7 +416,8 @@ def main():
     scan_ms = mean_ms(ev, 1, 2)  # side stream: concurrent with decode
     dec_call_ms = mean_ms(ev, 1, 3) if scan and args.scan == "side" else mean_ms(ev, 2, 3)  # + memset, offsets
     enc_ms, dec_ms = mean_ms(ev, 4, 5), mean_ms(ev, 6, 7)  # the kernels alone
-    assert codec.error() == 0
+    if codec.error():
+        raise SystemExit(f"device error {codec.error()} during the timed steps")
 
     ms_per_step = wall * 1e3 / args.steps
     value = world * n / (wall / args.steps) / 1e9

@@ -17,6 +17,13 @@ def _round16(n: int) -> int:
     return max(16, (n + 15) // 16 * 16)
 
 
+def _check_input(x: torch.Tensor, n: int) -> None:
+    """The kernels read n bytes from x's device pointer: u8, contiguous, >= n."""
+    if x.dtype != torch.uint8 or not x.is_contiguous() or x.numel() < n or not x.is_cuda:
+        raise ValueError(f"input must be a contiguous uint8 device tensor of >= {n} bytes "
+                         f"(got {x.dtype}, {tuple(x.shape)}, contiguous={x.is_contiguous()}, {x.device})")
+
+
 def _stream_handle(stream: torch.cuda.Stream | None) -> int:
     s = stream if stream is not None else torch.cuda.current_stream()
     return int(s.cuda_stream)
@@ -40,7 +47,7 @@ class FLDevice:
         self.out = torch.empty(_round16(n), dtype=torch.uint8, device=dev)
 
     def encode(self, x: torch.Tensor, stream: torch.cuda.Stream | None = None) -> None:
-        assert x.dtype == torch.uint8 and x.is_contiguous() and x.numel() >= self.n
+        _check_input(x, self.n)
         flrl.fl_encode_device(x.data_ptr(), self.n, self.bits.data_ptr(), self.values.data_ptr(),
                               self.sizes.data_ptr() + 8, self.scratch.data_ptr(),
                               self.scratch_bytes, _stream_handle(stream))
@@ -82,7 +89,7 @@ class RLDevice:
         self.out = torch.empty(_round16(n), dtype=torch.uint8, device=dev)
 
     def encode(self, x: torch.Tensor, stream: torch.cuda.Stream | None = None) -> None:
-        assert x.dtype == torch.uint8 and x.is_contiguous() and x.numel() >= self.n
+        _check_input(x, self.n)
         flrl.rl_encode_device(x.data_ptr(), self.n, self.counts.data_ptr(), self.values.data_ptr(),
                               self.runs_t.data_ptr(), self.scratch.data_ptr(), self.scratch_bytes,
                               _stream_handle(stream))
