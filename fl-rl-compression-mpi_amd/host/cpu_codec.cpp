@@ -94,15 +94,21 @@ flrl_fl_buf cpuCompressFL(const uint8_t *data, size_t n, unsigned threads)
             c.bits[f] = (uint8_t)b;
         }
     });
-    std::vector<uint64_t> off(F);
-    uint64_t acc = 0;
-    for (size_t f = 0; f < F; ++f) {
-        off[f] = 16 * acc;
-        acc += c.bits[f];
+    std::vector<uint64_t> off;
+    try {
+        off.resize(F);
+        uint64_t acc = 0;
+        for (size_t f = 0; f < F; ++f) {
+            off[f] = 16 * acc;
+            acc += c.bits[f];
+        }
+        const size_t cnt_last = n - (F - 1) * kFrame;
+        c.values_size = off[F - 1] + (cnt_last * c.bits[F - 1] + 7) / 8;
+        c.values = alloc_bytes(c.values_size);
+    } catch (...) {  // the caller gets nothing to free
+        std::free(c.bits);
+        throw;
     }
-    const size_t cnt_last = n - (F - 1) * kFrame;
-    c.values_size = off[F - 1] + (cnt_last * c.bits[F - 1] + 7) / 8;
-    c.values = alloc_bytes(c.values_size);
     parallel_for(F, threads, [&](size_t lo, size_t hi) {
         for (size_t f = lo; f < hi; ++f) {
             const unsigned b = c.bits[f];
