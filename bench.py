@@ -162,6 +162,10 @@ def mean_ms(ev, a: int, b: int) -> float:
     return float(np.mean([e[a].elapsed_time(e[b]) for e in ev]))
 
 
+def median_ms(ev, a: int, b: int) -> float:
+    return float(np.median([e[a].elapsed_time(e[b]) for e in ev]))
+
+
 def north_star_section(seed: int, steps: int, warmup: int, dev):
     """BASELINE north star: FL encode of 16 GiB uniform-random bytes on 1 GPU,
     target >= 70 % of HBM peak on algorithmic bytes. Encode and
@@ -206,9 +210,10 @@ def north_star_section(seed: int, steps: int, warmup: int, dev):
     alg = n + codec.frames + v
     res = {
         "workload": f"FL encode of {n} u8 bytes (seed {seed}) on 1 GPU (BASELINE north star)",
-        "timing": "kernel time (HIP events around the kernel, flrl_time_next_kernel); call = + scratch memset"
-                  " (decode: + offsets pre-pass)",
+        "timing": "kernel time (HIP events around the kernel, flrl_time_next_kernel); call = + scratch "
+                  "zero-fill (decode: + offsets pre-pass)",
         "encode_ms": round(enc_ms, 4),
+        "encode_median_ms": round(median_ms(ev, 2, 3), 4),
         "encode_call_ms": round(enc_call_ms, 4),
         "encode_alg_GBps": round(alg / (enc_ms * 1e-3) / 1e9, 1),
         "encode_input_GBps": round(n / (enc_ms * 1e-3) / 1e9, 1),
@@ -479,13 +484,15 @@ def main():
                 "algorithmic_bytes_per_launch": alg,
             },
             "kernels": {
-                "timing": "ms = the kernel alone (HIP events recorded by flrl_time_next_kernel on the "
-                          "launch stream); call_ms = the whole device call (+ scratch memset; decode: + "
-                          "offsets pre-pass)",
-                "fl_encode": {"ms": round(enc_ms, 4), "call_ms": round(enc_call_ms, 4),
+                "timing": "ms / median_ms = mean / median over K steps of the kernel alone (HIP events "
+                          "recorded by flrl_time_next_kernel on the launch stream); call_ms = the whole "
+                          "device call (+ scratch zero-fill; decode: + offsets pre-pass)",
+                "fl_encode": {"ms": round(enc_ms, 4), "median_ms": round(median_ms(ev, 4, 5), 4),
+                              "call_ms": round(enc_call_ms, 4),
                               "alg_GBps": round(enc_gbs, 1),
                               "input_GBps": round(n / (enc_ms * 1e-3) / 1e9, 1)},
-                "fl_decode": {"ms": round(dec_ms, 4), "call_ms": round(dec_call_ms, 4),
+                "fl_decode": {"ms": round(dec_ms, 4), "median_ms": round(median_ms(ev, 6, 7), 4),
+                              "call_ms": round(dec_call_ms, 4),
                               "alg_GBps": round(dec_gbs, 1),
                               "output_GBps": round(n / (dec_ms * 1e-3) / 1e9, 1)},
                 "size_scan": {"ms": round(scan_ms, 4), "stream": args.scan if scan else None},
