@@ -411,3 +411,45 @@ def test_graph_capture_replays(n):
         assert torch.equal(d.bits[: d.frames], bits0) and torch.equal(d.values[:v], vals0), i
         assert torch.equal(r.counts[:R], c0) and torch.equal(r.values[:R], rv0), i
         assert torch.equal(d.out[:n], x[:n]) and torch.equal(r.out[:n], x[:n]), i
+
+
+@pytest.mark.gpu
+def test_concurrent_streams():
+    """Two FL and two RL codecs on four streams at once: the persistent grids
+    compete for the CUs (workgroups dispatched late find every tile taken);
+    every output must still equal the one from a serial run."""
+    from flrl.device import FLDevice, RLDevice, gen
+    sizes = [(48 << 20) + 5, (40 << 20) + 131, (32 << 20) + 7, (24 << 20) + 9]
+    xs = [gen(k, n, 11 + i) for i, (k, n) in enumerate(zip(["u8", "lo4", "u8", "zero"], sizes))]
+    fl = [FLDevice(sizes[0]), FLDevice(sizes[1])]
+    rl = [RLDevice(sizes[2]), RLDevice(sizes[3])]
+    ref = []
+    for d, x in zip(fl, xs[:2]):
+        d.encode(x)
+        v = d.values_size()
+        ref.append((v, d.bits[: d.frames].clone(), d.values[:v].clone()))
+    for r, x in zip(rl, xs[2:]):
+        r.encode(x)
+        R = r.runs()
+        ref.append((R, r.counts[:R].clone(), r.values[:R].clone()))
+    torch.cuda.synchronize()
+    streams = [torch.cuda.Stream() for _ in range(4)]
+    for rep in range(5):
+        for t in (fl[0].out, fl[1].out, rl[0].out, rl[1].out):
+            t.zero_()
+        torch.cuda.synchronize()
+        for i in range(2):
+            fl[i].encode(xs[i], stream=streams[i])
+            fl[i].decode(ref[i][0], stream=streams[i])
+            rl[i].encode(xs[2 + i], stream=streams[2 + i])
+            rl[i].decode(ref[2 + i][0], stream=streams[2 + i])
+        torch.cuda.synchronize()
+        for i in range(2):
+            v, b0, v0 = ref[i]
+            assert fl[i].error() == 0 and fl[i].values_size() == v, (rep, i)
+            assert torch.equal(fl[i].bits[: fl[i].frames], b0) and torch.equal(fl[i].values[:v], v0), (rep, i)
+            assert torch.equal(fl[i].out[: sizes[i]], xs[i][: sizes[i]]), (rep, i)
+            R, c0, rv0 = ref[2 + i]
+            assert rl[i].error() == 0 and rl[i].runs() == R, (rep, i)
+            assert torch.equal(rl[i].counts[:R], c0) and torch.equal(rl[i].values[:R], rv0), (rep, i)
+            assert torch.equal(rl[i].out[: sizes[2 + i]], xs[2 + i][: sizes[2 + i]]), (rep, i)
