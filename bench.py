@@ -13,8 +13,16 @@ Default workload = BASELINE.json configs[1]: FL encode/decode of 1 GiB of
 uniform-random bytes per GPU, bit-exact against the reference fl-cpu (the
 1 GiB output's sha256 is the reference's).
 
-Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 under
-torch.distributed.run (one rank per GPU; backend nccl = RCCL over xGMI).
+Every N-rank line also carries `configs4`: BASELINE configs[4], FL encode of
+16 GiB uniform-random bytes per GPU through flrl_fl_encode_rank (encode + the
+RCCL size exchange), 128 GiB at N = 8. At N = 1 the same workload is the
+`north_star` section.
+
+Launch: python bench.py [--gpus N --steps K --warmup W]. For N > 1 the ranks
+are started by this script (torch.distributed.run child, one rank per GPU)
+unless it already runs under torch.distributed.run. The data-path exchange is
+an RCCL communicator of the C ABI (flrl_comm_init_rank, xGMI); torch.distributed
+(gloo) carries only the unique id, the barriers and the max-over-ranks timing.
 """
 from __future__ import annotations
 
@@ -23,11 +31,41 @@ import hashlib
 import struct
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "fl-rl-compression-mpi_amd"))
+
+
+def _gpus_arg(argv) -> int:
+    p = argparse.ArgumentParser(add_help=False)
+    p.add_argument("--gpus", type=int, default=1)
+    return p.parse_known_args(argv)[0].gpus
+
+
+def rank_launch_cmd(argv, env) -> list | None:
+    """`python bench.py --gpus N` (N > 1) outside torch.distributed: the command
+    that starts the N ranks (torch.distributed.run, one process per GPU,
+    127.0.0.1 rendezvous on a free port), run as a child process by this
+    process BEFORE anything touches the GPU (never an exec). None when this
+    process is itself a rank (WORLD_SIZE set) or N == 1."""
+    n = _gpus_arg(argv)
+    if n <= 1 or "WORLD_SIZE" in env:
+        return None
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *argv]
+
+
+if __name__ == "__main__":
+    _cmd = rank_launch_cmd(sys.argv[1:], os.environ)
+    if _cmd is not None:
+        sys.exit(subprocess.call(_cmd))
 
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
@@ -35,7 +73,6 @@ import torch.distributed as dist  # noqa: E402
 
 import flrl  # noqa: E402
 from flrl.device import FLDevice, RLDevice, gen  # noqa: E402
-from flrl.dist import size_scan  # noqa: E402
 
 METRIC = ("encode+decode GB/s (input bytes) at 1/2/4/8 GPUs; % HBM roofline; "
           "bit-exact round-trip")
@@ -56,14 +93,11 @@ def parse():
     p.add_argument("--traffic-json", default=None,
                    help="PMC summary (scripts/summarize_profile.py); default profiles/traffic_<kind>_<bytes>.json")
     p.add_argument("--no-north-star", action="store_true",
-                   help="skip the 16 GiB u8 FL encode (BASELINE north-star target) at N=1")
+                   help="skip the 16 GiB-per-GPU u8 FL encode (north star at N=1, configs[4] at N>1)")
     p.add_argument("--no-rl", action="store_true",
                    help="skip the RL section (config #3: 1 GiB runs32), which runs at N=1 only")
-    p.add_argument("--scan", default="inline", choices=["inline", "side"],
-                   help="size-scan (N > 1) between encode and decode, or on a side stream concurrent with the "
-                        "decode (measured slower: its small kernels take CUs from the persistent decode)")
     p.add_argument("--force-scan", action="store_true",
-                   help="run the RCCL size-scan even at N = 1 (under torch.distributed.run; testing)")
+                   help="run the RCCL size exchange (flrl_fl_encode_rank, 1-rank comm) even at N = 1")
     return p.parse_args()
 
 
@@ -297,6 +331,84 @@ def rl_section(n: int, seed: int, steps: int, warmup: int, dev, cpu: bool):
     return res
 
 
+def configs4_section(comm, rank: int, world: int, seed: int, steps: int, warmup: int, dev):
+    """BASELINE configs[4]: FL encode of 16 GiB uniform-random bytes per GPU
+    (128 GiB at N = 8), rank r holding global bytes [r*16 GiB, (r+1)*16 GiB),
+    through flrl_fl_encode_rank (encode + the RCCL all-gather of {F_r, V_r} +
+    device scan). K uninstrumented steps between barriers, max over ranks; then
+    K steps with HIP events around each rank's encode kernel. Parity: every
+    rank's device round trip, every rank's exchange record against the ranks'
+    sizes, and rank 0's first 1 GiB against the reference fl-cpu hash."""
+    n = 16 << 30
+    x = gen("u8", n, seed, word_offset=rank * n // 8, device=dev)
+    codec = FLDevice(n, dev)
+    stream = torch.cuda.current_stream()
+    for _ in range(max(1, warmup)):
+        codec.encode_rank(comm, x)
+    torch.cuda.synchronize()
+    rec = [int(t) for t in codec.rank_sizes[:flrl.SZ_COUNT].cpu()]
+    err = codec.error()
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        codec.encode_rank(comm, x)
+    torch.cuda.synchronize()
+    dist.barrier()
+    wall = time.perf_counter() - t0
+    ev = created_events(steps, 2, stream)
+    torch.cuda.synchronize()
+    for k in range(steps):
+        flrl.time_next_kernel(ev[k][0], ev[k][1])
+        codec.encode_rank(comm, x)
+    torch.cuda.synchronize()
+    enc_ms = mean_ms(ev, 0, 1)
+    v = rec[flrl.SZ_V]
+    prefix_ok = None
+    if rank == 0:
+        f1 = (1 << 30) // 128
+        v1 = int(codec.bits[:f1].to(torch.int64).sum().item()) * 16
+        h = hashlib.sha256(struct.pack("<QQQ", 1 << 30, f1, v1))
+        h.update(codec.bits[:f1].cpu().numpy().tobytes())
+        h.update(codec.values[:v1].cpu().numpy().tobytes())
+        prefix_ok = seed == 42 and h.hexdigest() == GOLDEN_1GIB_U8_SHA
+    out = torch.empty_like(x)
+    codec.decode(v, out=out)
+    ok = bool(torch.equal(out, x)) and err == 0 and codec.error() == 0
+    del out
+    alg = n + codec.frames + v
+    mine = {"rank": rank, "wall": wall, "encode_ms": enc_ms, "F": rec[flrl.SZ_F], "V": v,
+            "F_off": rec[flrl.SZ_F_OFF], "V_off": rec[flrl.SZ_V_OFF],
+            "F_total": rec[flrl.SZ_F_TOTAL], "V_total": rec[flrl.SZ_V_TOTAL],
+            "frac": alg / (enc_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, "roundtrip": ok}
+    allr = [None] * world
+    dist.all_gather_object(allr, mine)
+    del x, codec
+    torch.cuda.empty_cache()
+    if rank != 0:
+        return None
+    Fs = [r["F"] for r in allr]
+    Vs = [r["V"] for r in allr]
+    scan_ok = all(r["F_off"] == sum(Fs[:i]) and r["V_off"] == sum(Vs[:i]) and r["F_total"] == sum(Fs)
+                  and r["V_total"] == sum(Vs) and r["F"] == n // 128 for i, r in enumerate(allr))
+    wall = max(r["wall"] for r in allr)
+    return {
+        "workload": f"BASELINE configs[4]: FL encode of {n} u8 bytes per GPU x{world} = {n * world} bytes "
+                    f"(seed {seed}), flrl_fl_encode_rank (encode + RCCL size exchange)",
+        "ranks_seen": world,
+        "value": round(world * n / (wall / steps) / 1e9, 2),
+        "unit": "GB/s (input bytes, whole job)",
+        "ms_per_step": round(wall * 1e3 / steps, 4),
+        "per_rank_encode_ms": [round(r["encode_ms"], 4) for r in allr],
+        "per_rank_frac": [round(r["frac"], 4) for r in allr],
+        "min_frac": round(min(r["frac"] for r in allr), 4),
+        "size_scan_ok": scan_ok,
+        "roundtrip": all(r["roundtrip"] for r in allr),
+        "prefix_1GiB_matches_reference_fl_cpu": prefix_ok,
+        "F_total": allr[0]["F_total"], "V_total": allr[0]["V_total"],
+    }
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -305,10 +417,23 @@ def main():
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     torch.cuda.set_device(local)
-    scan = world > 1 or args.force_scan
-    if scan:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
+    scan = world > 1 or args.force_scan
+    comm = None
+    if world > 1:
+        # control plane only (unique id, barriers, max over ranks); the data
+        # path's exchange is the C ABI's own RCCL communicator
+        dist.init_process_group("gloo")
+        uid = [flrl.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        comm = flrl.Comm.rank(world, uid[0], rank)
+    elif scan:
+        comm = flrl.Comm.rank(1, flrl.comm_unique_id(), 0)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
     n = args.bytes
     if n % 128:
         raise SystemExit("--bytes must be a multiple of 128 (frame-aligned shards for weak scaling)")
@@ -318,9 +443,16 @@ def main():
     out = torch.empty_like(x)
     stream = torch.cuda.current_stream()
 
+    def encode():
+        if scan:
+            codec.encode_rank(comm, x)
+        else:
+            codec.encode(x)
+
     # ---- correctness of this exact workload (outside the timed region) ----
-    codec.encode(x)
-    v = codec.values_size()
+    encode()
+    torch.cuda.synchronize()
+    v = int(codec.rank_sizes[flrl.SZ_V].item()) if scan else codec.values_size()
     err = codec.error()
     codec.decode(v, out=out)
     err |= codec.error()
@@ -334,49 +466,34 @@ def main():
         parity["fl_sha256"] = sha
         if args.kind == "u8" and args.seed == 42 and n == 1 << 30:
             parity["fl_sha256_matches_reference_fl_cpu"] = sha == GOLDEN_1GIB_U8_SHA
+    if scan:  # the exchange record, checked against every rank's sizes
+        rec = [int(t) for t in codec.rank_sizes[:flrl.SZ_COUNT].cpu()]
+        allv = [None] * world
+        if world > 1:
+            dist.all_gather_object(allv, (rec[flrl.SZ_F], rec[flrl.SZ_V]))
+        else:
+            allv = [(rec[flrl.SZ_F], rec[flrl.SZ_V])]
+        parity["size_scan_ok"] = bool(
+            rec[flrl.SZ_F] == codec.frames and rec[flrl.SZ_V] == v
+            and rec[flrl.SZ_F_OFF] == sum(a[0] for a in allv[:rank])
+            and rec[flrl.SZ_V_OFF] == sum(a[1] for a in allv[:rank])
+            and rec[flrl.SZ_F_TOTAL] == sum(a[0] for a in allv)
+            and rec[flrl.SZ_V_TOTAL] == sum(a[1] for a in allv))
 
-    # The size-scan (RCCL all-gather of {F_r, V_r} + exclusive scan) places each
-    # shard's output; this rank's decode does not depend on it. --scan side runs
-    # it on a side stream concurrent with the decode (the step ends when both are
-    # done: the next encode rewrites the sizes the all-gather reads); measured
-    # slower than inline at N = 1 (0.829 vs 0.800 ms/step), so inline is default.
-    side = torch.cuda.Stream(device=dev)
-
+    # One step: encode (+ the exchange when scan: flrl_fl_encode_rank runs the
+    # RCCL all-gather of {F_r, V_r} and the scan on the same stream), decode.
     def step(e=None):
         if e is not None:
             e[0].record(stream)
             flrl.time_next_kernel(e[4], e[5])
-        codec.encode(x)
+        encode()
         if e is not None:
             e[1].record(stream)
-        if scan and args.scan == "side":
-            side.wait_stream(stream)
-            with torch.cuda.stream(side):
-                size_scan(codec.sizes)
-                if e is not None:
-                    e[2].record(side)
-        elif scan:
-            size_scan(codec.sizes)
-            if e is not None:
-                e[2].record(stream)
-        elif e is not None:
             e[2].record(stream)
-        if e is not None:
             flrl.time_next_kernel(e[6], e[7])
         codec.decode(v, out=out)
         if e is not None:
             e[3].record(stream)
-        if scan and args.scan == "side":
-            stream.wait_stream(side)
-
-    if scan:  # the size-scan's result, checked once against the ranks' sizes
-        offs, totals = size_scan(codec.sizes)
-        allv = [torch.empty_like(codec.sizes) for _ in range(world)]
-        dist.all_gather(allv, codec.sizes)
-        allv = torch.stack(allv).cpu()
-        parity["size_scan_ok"] = bool(
-            int(offs[0]) == int(allv[:rank, 0].sum()) and int(offs[1]) == int(allv[:rank, 1].sum())
-            and int(totals[0]) == int(allv[:, 0].sum()) and int(totals[1]) == int(allv[:, 1].sum()))
 
     # ---- warmup ----
     for _ in range(args.warmup):
@@ -395,31 +512,28 @@ def main():
 
     # ---- timed region: K uninstrumented steps (a timing event costs ~4.6 us of GPU
     # timeline, scripts/event_cost.py: 8 per step would add ~5 %) ----
-    if scan:
-        dist.barrier()
+    barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(args.steps):
         step()
     torch.cuda.synchronize()
-    if scan:
-        dist.barrier()
+    barrier()
     wall = time.perf_counter() - t0
-    if scan:
-        t = torch.tensor([wall], dtype=torch.float64, device=dev)
+    if world > 1:
+        t = torch.tensor([wall], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         wall = float(t.item())
 
     # ---- per-kernel breakdown: K more steps with HIP events (not part of `value`) ----
-    # 0-3: step phases (encode call, size-scan, decode call); 4-7: encode / decode kernels alone
+    # 0-3: step phases (encode call incl. exchange, -, decode call); 4-7: encode / decode kernels alone
     ev = created_events(args.steps, 8, stream)
     torch.cuda.synchronize()
     for k in range(args.steps):
         step(ev[k])
     torch.cuda.synchronize()
-    enc_call_ms = mean_ms(ev, 0, 1)  # + scratch memset
-    scan_ms = mean_ms(ev, 1, 2)  # side stream: concurrent with decode
-    dec_call_ms = mean_ms(ev, 1, 3) if scan and args.scan == "side" else mean_ms(ev, 2, 3)  # + memset, offsets
+    enc_call_ms = mean_ms(ev, 0, 1)  # + scratch zero-fill (+ the exchange when scan)
+    dec_call_ms = mean_ms(ev, 2, 3)  # + zero-fill, offsets pre-pass
     enc_ms, dec_ms = mean_ms(ev, 4, 5), mean_ms(ev, 6, 7)  # the kernels alone
     if codec.error():
         raise SystemExit(f"device error {codec.error()} during the timed steps")
@@ -435,11 +549,17 @@ def main():
     achieved = enc_gbs if dominant == "fl_encode" else dec_gbs
     traffic = pmc_traffic(args.kind, n, dominant, args.traffic_json)
 
-    if scan:
+    if world > 1:
         for key in ("roundtrip", "size_scan_ok"):
-            ok = torch.tensor([1 if parity[key] else 0], device=dev)
+            ok = torch.tensor([1 if parity[key] else 0])
             dist.all_reduce(ok, op=dist.ReduceOp.MIN)
             parity[key] = bool(ok.item())
+    del x, out, codec
+    torch.cuda.empty_cache()
+
+    c4 = None
+    if world > 1 and not args.no_north_star:
+        c4 = configs4_section(comm, rank, world, args.seed, args.steps, args.warmup, dev)
 
     if rank == 0:
         cpu = None
@@ -469,9 +589,11 @@ def main():
                 "workload": f"FL encode+decode of {n} {args.kind} bytes per GPU ({workload_ref(n, args.kind, world)})",
                 "bytes_per_gpu": n,
                 "global_bytes": n * world,
-                "parallelism": f"dp{world}: 128-aligned shards, RCCL size-scan" if world > 1 else "single GPU",
+                "parallelism": (f"dp{world}: 128-aligned shards, RCCL size exchange (flrl_fl_encode_rank)"
+                                if world > 1 else "single GPU"),
+                "ranks_seen": world,
                 "values_size_per_gpu": v,
-                "ratio": round((codec.frames + v + 24) / n, 6),
+                "ratio": round((alg - n + 24) / n, 6),
             },
             "roofline": {
                 "bound": "hbm",
@@ -486,7 +608,8 @@ def main():
             "kernels": {
                 "timing": "ms / median_ms = mean / median over K steps of the kernel alone (HIP events "
                           "recorded by flrl_time_next_kernel on the launch stream); call_ms = the whole "
-                          "device call (+ scratch zero-fill; decode: + offsets pre-pass)",
+                          "device call (+ scratch zero-fill; + the size exchange when N > 1; decode: "
+                          "+ offsets pre-pass)",
                 "fl_encode": {"ms": round(enc_ms, 4), "median_ms": round(median_ms(ev, 4, 5), 4),
                               "call_ms": round(enc_call_ms, 4),
                               "alg_GBps": round(enc_gbs, 1),
@@ -495,7 +618,6 @@ def main():
                               "call_ms": round(dec_call_ms, 4),
                               "alg_GBps": round(dec_gbs, 1),
                               "output_GBps": round(n / (dec_ms * 1e-3) / 1e9, 1)},
-                "size_scan": {"ms": round(scan_ms, 4), "stream": args.scan if scan else None},
                 "device_copy_ceiling": {"ms": round(copy_ms, 4), "GBps": round(copy_gbs, 1),
                                         "note": "torch copy_ of the same N bytes (read N + write N)"},
             },
@@ -503,9 +625,12 @@ def main():
             "parity": parity,
             "rl": rl,
             "north_star": ns,
+            "configs4": c4,
         }
         print(json.dumps(line), flush=True)
-    if scan:
+    if comm is not None:
+        comm.destroy()
+    if world > 1:
         dist.destroy_process_group()
 
 

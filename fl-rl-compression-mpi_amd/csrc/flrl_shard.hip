@@ -1,221 +1,770 @@
-// flrl_shard.hip — sharded FL encode across the GPUs of one node, one process.
+// flrl_shard.hip — multi-GPU FL encode: RCCL communicators, the one exchange
+// step (an all-gather of {F_r, V_r} + exclusive scan) and the entry points
+// built on it.
 //
 // Replaces gpuNCCLCompress (src/fl/fl_gpu.cu:76-287) and gpuMPICompress
-// (:41-74). The reference runs one MPI rank per GPU, exchanges the three sizes
-// with MPI_Allgather, then ncclAllGather's every rank's padded outputs to every
-// rank (O(P*N) traffic) and concatenates on rank 0. Here one process drives all
-// GPUs: shards follow the reference rule (file_io.cu:46-51, in size_t: every
-// shard but the last is floor(N/(128P))*128 bytes), each GPU encodes its shard
-// in place, and a single RCCL ncclAllGather of {F_r, V_r} (16 B per GPU over
-// xGMI) gives every GPU the exclusive scan that places its bits/values in the
-// output. Concatenating 128-aligned shard outputs equals the whole-input output
-// byte for byte, so the result is identical to
-// flrl_fl_compress.
+// (:41-74). The reference runs one MPI rank per GPU, exchanges three sizes with
+// MPI_Allgather (:101-106), then ncclAllGather's every rank's padded outputs to
+// every rank (O(P*N) traffic, :144-194) and concatenates on rank 0. Here the
+// only collective on the data path is one RCCL ncclAllGather of 16 bytes per
+// shard over xGMI; every shard learns its output offsets {F_off, V_off} and the
+// totals on the device, with no host round trip. Concatenating 128-aligned
+// shard outputs equals the whole-input output byte for byte (SURVEY.md §0
+// fact 7), so placing shard r at its offsets reproduces flrl_fl_compress.
+//
+// Two process models:
+//  * one process per GPU (the reference's model, main.cu:46-70): a rank's comm
+//    from flrl_comm_init_rank / flrl_comm_wrap; flrl_fl_encode_rank encodes the
+//    rank's shard in place and runs the exchange on the caller's stream;
+//    flrl_fl_compress_rank is the host-buffer twin of gpuNCCLCompress (rank 0
+//    receives the merged result, ncclSend/ncclRecv of the payloads);
+//  * one process driving the node's GPUs: flrl_comm_init (ncclCommInitAll over
+//    distinct devices); flrl_fl_encode_sharded places shard r on device
+//    r mod ndev, so any number of shards runs on any number of GPUs: shards of
+//    one device exchange through a local slot array, devices through RCCL.
+// A comm is created once and reused by every call (no per-call
+// ncclCommInitAll); flrl_fl_compress_sharded keeps one per device set.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
-#include <thread>
+#include <map>
+#include <mutex>
 #include <vector>
 
 #include "flrl.h"
+#include "flrl_device.hpp"
 #include "flrl_internal.hpp"
 
 using namespace flrl;
 
 namespace {
 
-struct Shard {
-    int dev = 0;
-    size_t off = 0, len = 0, frames = 0;
-    hipStream_t stream = nullptr;
-    void *base = nullptr;  // one device allocation per shard
-    uint8_t *d_in = nullptr, *d_bits = nullptr, *d_vals = nullptr;
-    uint64_t *d_sizes = nullptr, *d_all = nullptr;
-    void *d_scr = nullptr;
-    size_t scr_b = 0;
-    uint64_t vsize = 0;
-    int rc = 0;
-    char err[256] = {0};
+constexpr int kMaxLocal = 64;  // shards per device in one flrl_fl_encode_sharded call
+
+// Sizes record of every shard (include/flrl.h FLRL_SZ_*), written on the device.
+struct LocalOuts {
+    uint32_t count;
+    uint32_t index[kMaxLocal];   // global shard index
+    uint64_t *sizes[kMaxLocal];  // its d_sizes (FLRL_SZ_COUNT u64)
 };
 
-int shard_encode(Shard &s, const uint8_t *data, int ngpus)
+__global__ void put_u64_kernel(uint64_t *p, uint64_t v)
 {
-    if (hipSetDevice(s.dev) != hipSuccess)
-        return set_error(FLRL_E_HIP, "hipSetDevice(%d) failed", s.dev);
-    const size_t in_b = round_up(s.len ? s.len : 1, 16), bits_b = round_up(s.frames + 1, 16);
-    const size_t val_b = flrl_fl_values_capacity(s.len);
-    const size_t sizes_b = round_up(16 + 16 * (size_t)ngpus, 16);
-    s.scr_b = flrl_fl_scratch_bytes(s.len);
-    if (hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking) != hipSuccess)
-        return set_error(FLRL_E_HIP, "hipStreamCreate failed on device %d", s.dev);
-    if (hipMalloc(&s.base, in_b + bits_b + val_b + sizes_b + s.scr_b) != hipSuccess)
-        return set_error(FLRL_E_NOMEM, "Cannot allocate memory (device %d)", s.dev);
-    uint8_t *p = static_cast<uint8_t *>(s.base);
-    s.d_in = p;
-    s.d_bits = p + in_b;
-    s.d_vals = p + in_b + bits_b;
-    s.d_sizes = reinterpret_cast<uint64_t *>(p + in_b + bits_b + val_b);
-    s.d_all = s.d_sizes + 2;
-    s.d_scr = p + in_b + bits_b + val_b + sizes_b;
-    if (s.len && hipMemcpyAsync(s.d_in, data + s.off, s.len, hipMemcpyHostToDevice, s.stream) !=
-                     hipSuccess)
-        return set_error(FLRL_E_HIP, "shard upload failed on device %d", s.dev);
-    int rc = flrl_fl_encode_device(s.d_in, s.len, s.d_bits, s.d_vals, s.d_sizes + 1, s.d_scr,
-                                   s.scr_b, s.stream);
+    if (threadIdx.x == 0 && blockIdx.x == 0)
+        *p = v;
+}
+
+// gather holds {F, V} of shard r at slot ((r % ndev) * S + r / ndev) * 2 (the
+// all-gathered per-device slot arrays). Each thread owns one local shard: its
+// exclusive prefix over shards 0..r-1 in global order, and the totals.
+__global__ __launch_bounds__(kWave) void size_scan_kernel(const uint64_t *gather, uint32_t nshards,
+                                                          uint32_t ndev, uint32_t S, LocalOuts outs)
+{
+    const uint32_t t = threadIdx.x;
+    for (uint32_t i = t; i < outs.count; i += blockDim.x) {
+        const uint32_t me = outs.index[i];
+        uint64_t F = 0, V = 0, Fo = 0, Vo = 0, Fr = 0, Vr = 0;
+        for (uint32_t r = 0; r < nshards; ++r) {
+            const uint64_t *g = gather + ((uint64_t)(r % ndev) * S + r / ndev) * 2;
+            const uint64_t f = g[0], v = g[1];
+            if (r == me) {
+                Fo = F;
+                Vo = V;
+                Fr = f;
+                Vr = v;
+            }
+            F += f;
+            V += v;
+        }
+        uint64_t *o = outs.sizes[i];
+        o[FLRL_SZ_F] = Fr;
+        o[FLRL_SZ_V] = Vr;
+        o[FLRL_SZ_F_OFF] = Fo;
+        o[FLRL_SZ_V_OFF] = Vo;
+        o[FLRL_SZ_F_TOTAL] = F;
+        o[FLRL_SZ_V_TOTAL] = V;
+    }
+}
+
+struct Dev {
+    int id = 0;
+    ncclComm_t nccl = nullptr;
+    hipStream_t cstream = nullptr;  // exchange stream of the sharded path
+    hipEvent_t cdone = nullptr;
+    uint64_t *gather = nullptr;
+    size_t gather_cap = 0;          // u64 entries
+    std::vector<hipEvent_t> ev;     // per local shard slot
+};
+
+int rccl_error(ncclResult_t r, const char *what)
+{
+    return set_error(FLRL_E_RCCL, "%s failed: %s", what, ncclGetErrorString(r));
+}
+
+}  // namespace
+
+struct flrl_comm {
+    int nranks = 0, rank = 0;  // RCCL ranks of this process's view
+    bool owns = true;          // ncclCommDestroy on destroy (not for wrapped comms)
+    std::vector<Dev> dev;      // one per local device
+    std::mutex mu;             // calls on one comm are serialised
+};
+
+namespace {
+
+int dev_setup(Dev &d, size_t gather_entries)
+{
+    if (hipSetDevice(d.id) != hipSuccess)
+        return set_error(FLRL_E_HIP, "hipSetDevice(%d) failed", d.id);
+    if (!d.cstream && hipStreamCreateWithFlags(&d.cstream, hipStreamNonBlocking) != hipSuccess)
+        return set_error(FLRL_E_HIP, "hipStreamCreate failed on device %d", d.id);
+    if (!d.cdone && hipEventCreateWithFlags(&d.cdone, hipEventDisableTiming) != hipSuccess)
+        return set_error(FLRL_E_HIP, "hipEventCreate failed on device %d", d.id);
+    if (gather_entries > d.gather_cap) {
+        if (d.gather) {  // the previous call's exchange may still read it
+            (void)hipStreamSynchronize(d.cstream);
+            (void)hipFree(d.gather);
+            d.gather = nullptr;
+            d.gather_cap = 0;
+        }
+        if (hipMalloc(&d.gather, gather_entries * sizeof(uint64_t)) != hipSuccess)
+            return set_error(FLRL_E_NOMEM, "Cannot allocate memory (device %d)", d.id);
+        d.gather_cap = gather_entries;
+        if (hipMemset(d.gather, 0, gather_entries * sizeof(uint64_t)) != hipSuccess)
+            return set_error(FLRL_E_HIP, "hipMemset failed on device %d", d.id);
+    }
+    return FLRL_OK;
+}
+
+void dev_release(Dev &d, bool destroy_nccl)
+{
+    (void)hipSetDevice(d.id);
+    if (d.cstream)
+        (void)hipStreamSynchronize(d.cstream);
+    if (d.gather)
+        (void)hipFree(d.gather);
+    for (hipEvent_t e : d.ev)
+        (void)hipEventDestroy(e);
+    if (d.cdone)
+        (void)hipEventDestroy(d.cdone);
+    if (d.cstream)
+        (void)hipStreamDestroy(d.cstream);
+    if (destroy_nccl && d.nccl)
+        (void)ncclCommDestroy(d.nccl);
+    d = Dev{};
+}
+
+int device_of(const void *p, int *dev)
+{
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();  // not sticky for the next launch check
+        return -1;
+    }
+    if (a.type != hipMemoryTypeDevice && a.type != hipMemoryTypeManaged)
+        return -1;  // host memory (registered or not) is not a shard buffer
+    *dev = a.device;
+    return 0;
+}
+
+int current_device()
+{
+    int d = 0;
+    if (hipGetDevice(&d) != hipSuccess)
+        d = 0;
+    return d;
+}
+
+}  // namespace
+
+// ---- communicators ----------------------------------------------------------
+
+extern "C" int flrl_comm_init(int ndev, const int *devs, flrl_comm **out)
+{
+    clear_error();
+    if (!out)
+        return set_error(FLRL_E_ARG, "flrl_comm_init: null output");
+    *out = nullptr;
+    const int visible = flrl_device_count();
+    if (visible <= 0)
+        return set_error(FLRL_E_NODEV, "flrl_comm_init: no HIP device");
+    if (ndev <= 0)
+        ndev = visible;
+    std::vector<int> ids((size_t)ndev);
+    for (int i = 0; i < ndev; ++i) {
+        ids[(size_t)i] = devs ? devs[i] : i;
+        if (ids[(size_t)i] < 0 || ids[(size_t)i] >= visible)
+            return set_error(FLRL_E_ARG, "flrl_comm_init: device %d not visible (%d devices)",
+                             ids[(size_t)i], visible);
+        for (int j = 0; j < i; ++j)
+            if (ids[(size_t)j] == ids[(size_t)i])
+                return set_error(FLRL_E_ARG, "flrl_comm_init: device %d listed twice",
+                                 ids[(size_t)i]);
+    }
+    const int prev = current_device();
+    flrl_comm *c = new flrl_comm;
+    c->nranks = ndev;
+    c->rank = 0;
+    c->dev.resize((size_t)ndev);
+    std::vector<ncclComm_t> comms((size_t)ndev);
+    ncclResult_t r = ncclCommInitAll(comms.data(), ndev, ids.data());
+    if (r != ncclSuccess) {
+        delete c;
+        (void)hipSetDevice(prev);
+        return rccl_error(r, "ncclCommInitAll");
+    }
+    int rc = FLRL_OK;
+    for (int i = 0; i < ndev; ++i) {
+        c->dev[(size_t)i].id = ids[(size_t)i];
+        c->dev[(size_t)i].nccl = comms[(size_t)i];
+        if (rc == FLRL_OK)
+            rc = dev_setup(c->dev[(size_t)i], 2 * (size_t)ndev);
+    }
+    (void)hipSetDevice(prev);
+    if (rc) {
+        (void)flrl_comm_destroy(c);
+        return rc;
+    }
+    *out = c;
+    return FLRL_OK;
+}
+
+extern "C" int flrl_comm_unique_id(void *id)
+{
+    clear_error();
+    if (!id)
+        return set_error(FLRL_E_ARG, "flrl_comm_unique_id: null buffer");
+    static_assert(sizeof(ncclUniqueId) == FLRL_UNIQUE_ID_BYTES, "unique id size");
+    ncclUniqueId u;
+    const ncclResult_t r = ncclGetUniqueId(&u);
+    if (r != ncclSuccess)
+        return rccl_error(r, "ncclGetUniqueId");
+    memcpy(id, &u, sizeof(u));
+    return FLRL_OK;
+}
+
+extern "C" int flrl_comm_init_rank(int nranks, const void *id, int rank, flrl_comm **out)
+{
+    clear_error();
+    if (!out || !id)
+        return set_error(FLRL_E_ARG, "flrl_comm_init_rank: null argument");
+    *out = nullptr;
+    if (nranks <= 0 || rank < 0 || rank >= nranks)
+        return set_error(FLRL_E_ARG, "flrl_comm_init_rank: rank %d of %d", rank, nranks);
+    if (flrl_device_count() <= 0)
+        return set_error(FLRL_E_NODEV, "flrl_comm_init_rank: no HIP device");
+    ncclUniqueId u;
+    memcpy(&u, id, sizeof(u));
+    ncclComm_t nc = nullptr;
+    const ncclResult_t r = ncclCommInitRank(&nc, nranks, u, rank);  // on the current device
+    if (r != ncclSuccess)
+        return rccl_error(r, "ncclCommInitRank");
+    flrl_comm *c = new flrl_comm;
+    c->nranks = nranks;
+    c->rank = rank;
+    c->dev.resize(1);
+    c->dev[0].id = current_device();
+    c->dev[0].nccl = nc;
+    const int rc = dev_setup(c->dev[0], 2 * (size_t)nranks);
+    if (rc) {
+        (void)flrl_comm_destroy(c);
+        return rc;
+    }
+    *out = c;
+    return FLRL_OK;
+}
+
+extern "C" int flrl_comm_wrap(void *nccl_comm, flrl_comm **out)
+{
+    clear_error();
+    if (!out || !nccl_comm)
+        return set_error(FLRL_E_ARG, "flrl_comm_wrap: null argument");
+    *out = nullptr;
+    ncclComm_t nc = static_cast<ncclComm_t>(nccl_comm);
+    int n = 0, r = 0, d = 0;
+    ncclResult_t e;
+    if ((e = ncclCommCount(nc, &n)) != ncclSuccess || (e = ncclCommUserRank(nc, &r)) != ncclSuccess ||
+        (e = ncclCommCuDevice(nc, &d)) != ncclSuccess)
+        return rccl_error(e, "flrl_comm_wrap: communicator query");
+    const int prev = current_device();
+    flrl_comm *c = new flrl_comm;
+    c->nranks = n;
+    c->rank = r;
+    c->owns = false;
+    c->dev.resize(1);
+    c->dev[0].id = d;
+    c->dev[0].nccl = nc;
+    const int rc = dev_setup(c->dev[0], 2 * (size_t)n);
+    (void)hipSetDevice(prev);
+    if (rc) {
+        (void)flrl_comm_destroy(c);
+        return rc;
+    }
+    *out = c;
+    return FLRL_OK;
+}
+
+extern "C" int flrl_comm_destroy(flrl_comm *c)
+{
+    if (!c)
+        return FLRL_OK;
+    const int prev = current_device();
+    for (Dev &d : c->dev)
+        dev_release(d, c->owns);
+    (void)hipSetDevice(prev);
+    delete c;
+    return FLRL_OK;
+}
+
+extern "C" int flrl_comm_query(const flrl_comm *c, int *nranks, int *rank, int *ndev)
+{
+    if (!c)
+        return set_error(FLRL_E_ARG, "flrl_comm_query: null comm");
+    if (nranks)
+        *nranks = c->nranks;
+    if (rank)
+        *rank = c->rank;
+    if (ndev)
+        *ndev = (int)c->dev.size();
+    return FLRL_OK;
+}
+
+// ---- device-resident encode + exchange ------------------------------------
+
+extern "C" int flrl_fl_encode_rank(flrl_comm *c, const uint8_t *d_in, size_t n, uint8_t *d_bits,
+                                   uint8_t *d_values, uint64_t *d_sizes, void *d_scratch,
+                                   size_t scratch_bytes, void *stream)
+{
+    clear_error();
+    if (!c || !d_sizes)
+        return set_error(FLRL_E_ARG, "flrl_fl_encode_rank: null comm/sizes");
+    if (c->dev.size() != 1)
+        return set_error(FLRL_E_ARG,
+                         "flrl_fl_encode_rank: comm drives %zu devices (use flrl_fl_encode_sharded)",
+                         c->dev.size());
+    std::lock_guard<std::mutex> g(c->mu);
+    Dev &d = c->dev[0];
+    if (current_device() != d.id)
+        return set_error(FLRL_E_ARG, "flrl_fl_encode_rank: current device %d, comm on device %d",
+                         current_device(), d.id);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    // the previous call's scan may still read the gather array on another stream
+    FLRL_HIP(hipStreamWaitEvent(s, d.cdone, 0));
+    uint64_t *slot = d.gather + 2 * (size_t)c->rank;
+    hipLaunchKernelGGL(put_u64_kernel, dim3(1), dim3(kWave), 0, s, slot, (uint64_t)div_up(n, kFrame));
+    FLRL_HIP(hipGetLastError());
+    int rc = flrl_fl_encode_device(d_in, n, d_bits, d_values, slot + 1, d_scratch, scratch_bytes, stream);
     if (rc)
         return rc;
-    const uint64_t f = s.frames;
-    if (hipMemcpyAsync(s.d_sizes, &f, sizeof(f), hipMemcpyHostToDevice, s.stream) != hipSuccess)
-        return set_error(FLRL_E_HIP, "frame-count upload failed on device %d", s.dev);
-    if (hipStreamSynchronize(s.stream) != hipSuccess)  // also keeps &f alive for the copy
-        return set_error(FLRL_E_HIP, "stream sync failed on device %d", s.dev);
+    const ncclResult_t r = ncclAllGather(slot, d.gather, 2, ncclUint64, d.nccl, s);  // in place
+    if (r != ncclSuccess)
+        return rccl_error(r, "ncclAllGather");
+    LocalOuts outs{};
+    outs.count = 1;
+    outs.index[0] = (uint32_t)c->rank;
+    outs.sizes[0] = d_sizes;
+    hipLaunchKernelGGL(size_scan_kernel, dim3(1), dim3(kWave), 0, s, d.gather, (uint32_t)c->nranks,
+                       (uint32_t)c->nranks, 1u, outs);
+    FLRL_HIP(hipGetLastError());
+    FLRL_HIP(hipEventRecord(d.cdone, s));
+    return FLRL_OK;
+}
+
+extern "C" int flrl_fl_encode_sharded(flrl_comm *c, int nshards, const uint8_t *const *d_in,
+                                      const size_t *n, uint8_t *const *d_bits,
+                                      uint8_t *const *d_values, uint64_t *const *d_sizes,
+                                      void *const *d_scratch, const size_t *scratch_bytes,
+                                      void *const *streams)
+{
+    clear_error();
+    if (!c || nshards <= 0 || !d_in || !n || !d_bits || !d_values || !d_sizes || !d_scratch ||
+        !scratch_bytes || !streams)
+        return set_error(FLRL_E_ARG, "flrl_fl_encode_sharded: null argument");
+    if (c->rank != 0 || (size_t)c->nranks != c->dev.size())
+        return set_error(FLRL_E_ARG, "flrl_fl_encode_sharded: needs a flrl_comm_init communicator");
+    std::lock_guard<std::mutex> g(c->mu);
+    const size_t ndev = c->dev.size();
+    const size_t P = (size_t)nshards;
+    const size_t S = div_up(P, ndev);  // slots per device
+    if (S > (size_t)kMaxLocal)
+        return set_error(FLRL_E_ARG, "flrl_fl_encode_sharded: %d shards on %zu devices (max %d per device)",
+                         nshards, ndev, kMaxLocal);
+    const int prev = current_device();
+    // buffers of shard r must live on device r mod ndev
+    for (size_t r = 0; r < P; ++r) {
+        const int want = c->dev[r % ndev].id;
+        int got = -1;
+        if (!d_values[r] || !d_scratch[r] || !d_sizes[r] || device_of(d_values[r], &got) || got != want ||
+            device_of(d_scratch[r], &got) || got != want || device_of(d_sizes[r], &got) || got != want) {
+            (void)hipSetDevice(prev);
+            return set_error(FLRL_E_ARG, "flrl_fl_encode_sharded: shard %zu buffers must be on device %d",
+                             r, want);
+        }
+    }
+    int rc = FLRL_OK;
+    for (size_t k = 0; k < ndev && rc == FLRL_OK; ++k) {
+        Dev &d = c->dev[k];
+        rc = dev_setup(d, 2 * S * ndev);
+        while (rc == FLRL_OK && d.ev.size() < S) {
+            hipEvent_t e;
+            if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess)
+                rc = set_error(FLRL_E_HIP, "hipEventCreate failed on device %d", d.id);
+            else
+                d.ev.push_back(e);
+        }
+    }
+    // 1. every shard: F into its slot, encode (V lands in the slot), event
+    for (size_t r = 0; r < P && rc == FLRL_OK; ++r) {
+        Dev &d = c->dev[r % ndev];
+        const size_t slot_i = ((r % ndev) * S + r / ndev) * 2;
+        hipStream_t s = static_cast<hipStream_t>(streams[r]);
+        if (hipSetDevice(d.id) != hipSuccess) {
+            rc = set_error(FLRL_E_HIP, "hipSetDevice(%d) failed", d.id);
+            break;
+        }
+        // the previous call's scan may still read this device's gather array
+        if (hipStreamWaitEvent(s, d.cdone, 0) != hipSuccess) {
+            rc = set_error(FLRL_E_HIP, "flrl_fl_encode_sharded: event wait failed on device %d", d.id);
+            break;
+        }
+        hipLaunchKernelGGL(put_u64_kernel, dim3(1), dim3(kWave), 0, s, d.gather + slot_i,
+                           (uint64_t)div_up(n[r], kFrame));
+        if (hipGetLastError() != hipSuccess) {
+            rc = set_error(FLRL_E_HIP, "flrl_fl_encode_sharded: launch failed on device %d", d.id);
+            break;
+        }
+        rc = flrl_fl_encode_device(d_in[r], n[r], d_bits[r], d_values[r], d.gather + slot_i + 1,
+                                   d_scratch[r], scratch_bytes[r], streams[r]);
+        if (rc)
+            break;
+        hipEvent_t e = d.ev[r / ndev];
+        if (hipEventRecord(e, s) != hipSuccess || hipStreamWaitEvent(d.cstream, e, 0) != hipSuccess)
+            rc = set_error(FLRL_E_HIP, "flrl_fl_encode_sharded: event failed on device %d", d.id);
+    }
+    // 2. the exchange: each device's S slots to every device
+    if (rc == FLRL_OK) {
+        ncclResult_t r1 = ncclGroupStart(), r2 = ncclSuccess;
+        for (size_t k = 0; k < ndev && r1 == ncclSuccess; ++k) {
+            Dev &d = c->dev[k];
+            r1 = ncclAllGather(d.gather + k * S * 2, d.gather, 2 * S, ncclUint64, d.nccl, d.cstream);
+        }
+        r2 = ncclGroupEnd();
+        if (r1 != ncclSuccess || r2 != ncclSuccess)
+            rc = rccl_error(r1 != ncclSuccess ? r1 : r2, "ncclAllGather");
+    }
+    // 3. per device: offsets of its shards, then the shards' streams wait for them
+    for (size_t k = 0; k < ndev && rc == FLRL_OK; ++k) {
+        Dev &d = c->dev[k];
+        LocalOuts outs{};
+        for (size_t r = k; r < P; r += ndev) {
+            outs.index[outs.count] = (uint32_t)r;
+            outs.sizes[outs.count] = d_sizes[r];
+            ++outs.count;
+        }
+        if (hipSetDevice(d.id) != hipSuccess) {
+            rc = set_error(FLRL_E_HIP, "hipSetDevice(%d) failed", d.id);
+            break;
+        }
+        hipLaunchKernelGGL(size_scan_kernel, dim3(1), dim3(kWave), 0, d.cstream, d.gather,
+                           (uint32_t)P, (uint32_t)ndev, (uint32_t)S, outs);
+        if (hipGetLastError() != hipSuccess || hipEventRecord(d.cdone, d.cstream) != hipSuccess) {
+            rc = set_error(FLRL_E_HIP, "flrl_fl_encode_sharded: size scan failed on device %d", d.id);
+            break;
+        }
+        for (size_t r = k; r < P; r += ndev)
+            if (hipStreamWaitEvent(static_cast<hipStream_t>(streams[r]), d.cdone, 0) != hipSuccess)
+                rc = set_error(FLRL_E_HIP, "flrl_fl_encode_sharded: event wait failed");
+    }
+    (void)hipSetDevice(prev);
+    return rc;
+}
+
+// ---- host-buffer forms -------------------------------------------------------
+
+namespace {
+
+// Device buffers of one shard of a host-buffer call (freed after its stream).
+struct ShardBufs {
+    int dev = 0;
+    size_t off = 0, len = 0;
+    hipStream_t s = nullptr;
+    void *base = nullptr;
+    uint8_t *in = nullptr, *bits = nullptr, *vals = nullptr;
+    uint64_t *sizes = nullptr;
+    void *scr = nullptr;
+    size_t scr_b = 0;
+    int alloc(int device, size_t length)
+    {
+        dev = device;
+        len = length;
+        if (hipSetDevice(dev) != hipSuccess)
+            return set_error(FLRL_E_HIP, "hipSetDevice(%d) failed", dev);
+        if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess)
+            return set_error(FLRL_E_HIP, "hipStreamCreate failed on device %d", dev);
+        const size_t in_b = round_up(len ? len : 1, 16), bits_b = round_up(div_up(len, kFrame) + 1, 16);
+        const size_t val_b = flrl_fl_values_capacity(len), sz_b = 64;
+        scr_b = flrl_fl_scratch_bytes(len);
+        if (hipMalloc(&base, in_b + bits_b + val_b + sz_b + scr_b) != hipSuccess)
+            return set_error(FLRL_E_NOMEM, "Cannot allocate memory (device %d)", dev);
+        uint8_t *p = static_cast<uint8_t *>(base);
+        in = p;
+        bits = p + in_b;
+        vals = bits + bits_b;
+        sizes = reinterpret_cast<uint64_t *>(vals + val_b);
+        scr = vals + val_b + sz_b;
+        return FLRL_OK;
+    }
+    ~ShardBufs()  // after its stream has drained, on its own device
+    {
+        if (!s && !base)
+            return;
+        (void)hipSetDevice(dev);
+        if (s)
+            (void)hipStreamSynchronize(s);
+        if (base)
+            (void)hipFree(base);
+        if (s)
+            (void)hipStreamDestroy(s);
+    }
+};
+
+// One communicator per device count, created on first use and kept for the
+// life of the process (RCCL init costs ~100 ms; a comm per call made the
+// host-buffer sharded path unusable in a loop).
+flrl_comm *cached_comm(int ndev, int *rc)
+{
+    static std::mutex m;
+    static std::map<int, flrl_comm *> cache;
+    std::lock_guard<std::mutex> g(m);
+    auto it = cache.find(ndev);
+    if (it != cache.end())
+        return it->second;
+    flrl_comm *c = nullptr;
+    *rc = flrl_comm_init(ndev, nullptr, &c);
+    if (*rc)
+        return nullptr;
+    cache[ndev] = c;
+    return c;
+}
+
+int read_error(const ShardBufs &b, size_t r)
+{
+    (void)hipSetDevice(b.dev);
+    const int kerr = flrl_scratch_error(b.scr, b.s);
+    if (kerr)
+        return set_error(kerr, "shard %zu: device error %d", r, kerr);
     return FLRL_OK;
 }
 
 }  // namespace
 
-extern "C" int flrl_fl_compress_sharded(const uint8_t *data, size_t size, int ngpus,
+extern "C" int flrl_fl_compress_sharded(const uint8_t *data, size_t size, int nshards,
                                         flrl_fl_buf *out)
 {
     clear_error();
     if (!out || (!data && size))
         return set_error(FLRL_E_ARG, "flrl_fl_compress_sharded: null argument");
     memset(out, 0, sizeof(*out));
-    int ndev = flrl_device_count();
-    if (ndev <= 0)
+    const int visible = flrl_device_count();
+    if (visible <= 0)
         return set_error(FLRL_E_NODEV, "flrl_fl_compress_sharded: no HIP device");
-    if (ngpus <= 0)
-        ngpus = ndev;
-    if (ngpus > ndev)
-        return set_error(FLRL_E_ARG, "flrl_fl_compress_sharded: %d GPUs requested, %d visible",
-                         ngpus, ndev);
+    if (nshards <= 0)
+        nshards = visible;
+    if (nshards > kMaxLocal * visible)
+        return set_error(FLRL_E_ARG, "flrl_fl_compress_sharded: %d shards (max %d)", nshards,
+                         kMaxLocal * visible);
     if (size == 0)
         return FLRL_OK;
-
-    const size_t P = (size_t)ngpus;
-    const size_t per = (size / (FLRL_FRAME_LENGTH * P)) * FLRL_FRAME_LENGTH;
-    std::vector<Shard> sh(P);
-    for (size_t r = 0; r < P; ++r) {
-        sh[r].dev = (int)r;
-        sh[r].off = r * per;
-        sh[r].len = r + 1 == P ? size - (P - 1) * per : per;
-        sh[r].frames = div_up(sh[r].len, FLRL_FRAME_LENGTH);
-    }
-    auto cleanup = [&]() {
-        for (auto &s : sh) {
-            if (s.base) {
-                (void)hipSetDevice(s.dev);
-                (void)hipFree(s.base);
-            }
-            if (s.stream)
-                (void)hipStreamDestroy(s.stream);
-        }
-    };
-
-    {
-        std::vector<std::thread> th;
-        for (size_t r = 0; r < P; ++r)
-            th.emplace_back([&, r]() {
-                clear_error();
-                sh[r].rc = shard_encode(sh[r], data, ngpus);
-                if (sh[r].rc)  // the last-error string is per thread: keep the worker's
-                    snprintf(sh[r].err, sizeof(sh[r].err), "%s", flrl_last_error());
-            });
-        for (auto &t : th)
-            t.join();
-    }
-    for (size_t r = 0; r < P; ++r)
-        if (sh[r].rc) {
-            cleanup();
-            return set_error(sh[r].rc, "flrl_fl_compress_sharded: shard %zu encode failed%s%s", r,
-                             sh[r].err[0] ? ": " : "", sh[r].err);
-        }
-
-    // ---- the one exchange step: AllGather {F_r, V_r} over xGMI -------------
-    std::vector<ncclComm_t> comms(P);
-    std::vector<int> devs(P);
-    for (size_t r = 0; r < P; ++r)
-        devs[r] = (int)r;
-    if (ncclCommInitAll(comms.data(), ngpus, devs.data()) != ncclSuccess) {
-        cleanup();
-        return set_error(FLRL_E_RCCL, "ncclCommInitAll failed");
-    }
-    ncclResult_t nr = ncclGroupStart();
-    for (size_t r = 0; r < P && nr == ncclSuccess; ++r)
-        nr = ncclAllGather(sh[r].d_sizes, sh[r].d_all, 2, ncclUint64, comms[r], sh[r].stream);
-    ncclResult_t ne = ncclGroupEnd();
-    std::vector<uint64_t> all(2 * P);
+    const int ndev = nshards < visible ? nshards : visible;
     int rc = FLRL_OK;
-    if (nr != ncclSuccess || ne != ncclSuccess)
-        rc = set_error(FLRL_E_RCCL, "ncclAllGather failed: %s",
-                       ncclGetErrorString(nr != ncclSuccess ? nr : ne));
-    for (size_t r = 0; r < P && rc == FLRL_OK; ++r) {
-        (void)hipSetDevice(sh[r].dev);
-        if (hipStreamSynchronize(sh[r].stream) != hipSuccess)
-            rc = set_error(FLRL_E_HIP, "flrl_fl_compress_sharded: stream sync failed");
-        const int kerr = flrl_scratch_error(sh[r].d_scr, sh[r].stream);
-        if (kerr)
-            rc = set_error(kerr, "flrl_fl_compress_sharded: device error %d on shard %zu", kerr, r);
-    }
-    if (rc == FLRL_OK) {
-        (void)hipSetDevice(sh[0].dev);
-        if (hipMemcpy(all.data(), sh[0].d_all, 16 * P, hipMemcpyDeviceToHost) != hipSuccess)
-            rc = set_error(FLRL_E_HIP, "flrl_fl_compress_sharded: size read-back failed");
-    }
-    for (auto &c : comms)
-        (void)ncclCommDestroy(c);
-    if (rc) {
-        cleanup();
+    flrl_comm *c = cached_comm(ndev, &rc);
+    if (!c)
         return rc;
-    }
+    const int prev = current_device();
 
-    // exclusive scan of {F_r, V_r} -> output placement
-    std::vector<size_t> foff(P), voff(P);
-    size_t F = 0, V = 0;
-    for (size_t r = 0; r < P; ++r) {
-        foff[r] = F;
-        voff[r] = V;
-        F += all[2 * r];
-        V += all[2 * r + 1];
+    // the reference shard rule (file_io.cu:46-51), size_t: every shard but the
+    // last is floor(N/(128P))*128 bytes
+    const size_t P = (size_t)nshards;
+    const size_t per = (size / (kFrame * P)) * kFrame;
+    std::vector<ShardBufs> sb(P);
+    std::vector<const uint8_t *> in(P);
+    std::vector<size_t> len(P), scr_b(P);
+    std::vector<uint8_t *> bits(P), vals(P);
+    std::vector<uint64_t *> sizes(P);
+    std::vector<void *> scr(P), streams(P);
+    for (size_t r = 0; r < P && rc == FLRL_OK; ++r) {
+        const size_t L = r + 1 == P ? size - (P - 1) * per : per;
+        rc = sb[r].alloc(c->dev[r % (size_t)ndev].id, L);
+        if (rc)
+            break;
+        sb[r].off = r * per;
+        if (L && hipMemcpyAsync(sb[r].in, data + sb[r].off, L, hipMemcpyHostToDevice, sb[r].s) != hipSuccess)
+            rc = set_error(FLRL_E_HIP, "shard %zu upload failed", r);
+        in[r] = sb[r].in;
+        len[r] = L;
+        bits[r] = sb[r].bits;
+        vals[r] = sb[r].vals;
+        sizes[r] = sb[r].sizes;
+        scr[r] = sb[r].scr;
+        scr_b[r] = sb[r].scr_b;
+        streams[r] = sb[r].s;
     }
-    uint8_t *h_bits = static_cast<uint8_t *>(malloc(F ? F : 1));
-    uint8_t *h_vals = static_cast<uint8_t *>(malloc(V ? V : 1));
-    if (!h_bits || !h_vals) {
+    if (rc == FLRL_OK)
+        rc = flrl_fl_encode_sharded(c, nshards, in.data(), len.data(), bits.data(), vals.data(),
+                                    sizes.data(), scr.data(), scr_b.data(), streams.data());
+    std::vector<uint64_t> rec(P * FLRL_SZ_COUNT);
+    for (size_t r = 0; r < P && rc == FLRL_OK; ++r) {
+        (void)hipSetDevice(sb[r].dev);
+        if (hipMemcpyAsync(&rec[r * FLRL_SZ_COUNT], sb[r].sizes, FLRL_SZ_COUNT * 8, hipMemcpyDeviceToHost,
+                           sb[r].s) != hipSuccess ||
+            hipStreamSynchronize(sb[r].s) != hipSuccess)
+            rc = set_error(FLRL_E_HIP, "shard %zu: size read-back failed", r);
+        else
+            rc = read_error(sb[r], r);
+    }
+    uint8_t *h_bits = nullptr, *h_vals = nullptr;
+    size_t F = 0, V = 0;
+    if (rc == FLRL_OK) {
+        F = rec[FLRL_SZ_F_TOTAL];
+        V = rec[FLRL_SZ_V_TOTAL];
+        h_bits = static_cast<uint8_t *>(malloc(F ? F : 1));
+        h_vals = static_cast<uint8_t *>(malloc(V ? V : 1));
+        if (!h_bits || !h_vals)
+            rc = set_error(FLRL_E_NOMEM, "Cannot allocate memory");
+    }
+    for (size_t r = 0; r < P && rc == FLRL_OK; ++r) {
+        const uint64_t *q = &rec[r * FLRL_SZ_COUNT];
+        (void)hipSetDevice(sb[r].dev);
+        if ((q[FLRL_SZ_F] && hipMemcpy(h_bits + q[FLRL_SZ_F_OFF], sb[r].bits, q[FLRL_SZ_F],
+                                       hipMemcpyDeviceToHost) != hipSuccess) ||
+            (q[FLRL_SZ_V] && hipMemcpy(h_vals + q[FLRL_SZ_V_OFF], sb[r].vals, q[FLRL_SZ_V],
+                                       hipMemcpyDeviceToHost) != hipSuccess))
+            rc = set_error(FLRL_E_HIP, "flrl_fl_compress_sharded: copy-out of shard %zu failed", r);
+    }
+    sb.clear();  // every shard's stream drained before its buffers are freed
+    (void)hipSetDevice(prev);
+    if (rc) {
         free(h_bits);
         free(h_vals);
-        cleanup();
-        return set_error(FLRL_E_NOMEM, "Cannot allocate memory");
+        return rc;
     }
-    {
-        std::vector<std::thread> th;
-        for (size_t r = 0; r < P; ++r)
-            th.emplace_back([&, r]() {
-                Shard &s = sh[r];
-                (void)hipSetDevice(s.dev);
-                const size_t fr = all[2 * r], vr = all[2 * r + 1];
-                if ((fr && hipMemcpy(h_bits + foff[r], s.d_bits, fr, hipMemcpyDeviceToHost)) ||
-                    (vr && hipMemcpy(h_vals + voff[r], s.d_vals, vr, hipMemcpyDeviceToHost)))
-                    s.rc = FLRL_E_HIP;
-            });
-        for (auto &t : th)
-            t.join();
-    }
-    for (size_t r = 0; r < P; ++r)
-        if (sh[r].rc) {
-            free(h_bits);
-            free(h_vals);
-            cleanup();
-            return set_error(FLRL_E_HIP, "flrl_fl_compress_sharded: copy-out of shard %zu failed",
-                             r);
-        }
-    cleanup();
     out->bits = h_bits;
     out->bits_size = F;
     out->values = h_vals;
     out->values_size = V;
     out->input_size = size;
     return FLRL_OK;
+}
+
+extern "C" int flrl_fl_compress_rank(flrl_comm *c, const uint8_t *data, size_t size, flrl_fl_buf *out)
+{
+    clear_error();
+    if (!c || !out || (!data && size))
+        return set_error(FLRL_E_ARG, "flrl_fl_compress_rank: null argument");
+    memset(out, 0, sizeof(*out));
+    if (c->dev.size() != 1)
+        return set_error(FLRL_E_ARG, "flrl_fl_compress_rank: needs a per-rank communicator");
+    const int prev = current_device();
+    ShardBufs b;
+    int rc = b.alloc(c->dev[0].id, size);
+    if (rc == FLRL_OK && size &&
+        hipMemcpyAsync(b.in, data, size, hipMemcpyHostToDevice, b.s) != hipSuccess)
+        rc = set_error(FLRL_E_HIP, "flrl_fl_compress_rank: upload failed");
+    if (rc == FLRL_OK)
+        rc = flrl_fl_encode_rank(c, b.in, size, b.bits, b.vals, b.sizes, b.scr, b.scr_b, b.s);
+    const size_t R = (size_t)c->nranks;
+    std::vector<uint64_t> all(2 * R);
+    uint64_t rec[FLRL_SZ_COUNT] = {0};
+    if (rc == FLRL_OK) {
+        std::lock_guard<std::mutex> g(c->mu);
+        if (hipMemcpyAsync(rec, b.sizes, sizeof(rec), hipMemcpyDeviceToHost, b.s) != hipSuccess ||
+            hipMemcpyAsync(all.data(), c->dev[0].gather, 16 * R, hipMemcpyDeviceToHost, b.s) != hipSuccess ||
+            hipStreamSynchronize(b.s) != hipSuccess)
+            rc = set_error(FLRL_E_HIP, "flrl_fl_compress_rank: size read-back failed");
+    }
+    if (rc == FLRL_OK)
+        rc = read_error(b, (size_t)c->rank);
+    // the whole input's size (the reference all-gathers inputSize, fl_gpu.cu:105)
+    uint64_t total_n = 0;
+    if (rc == FLRL_OK) {
+        std::lock_guard<std::mutex> g(c->mu);
+        uint64_t *d_n = b.sizes + FLRL_SZ_COUNT;  // spare u64s of the sizes block
+        const uint64_t mine = size;
+        ncclResult_t r1;
+        if (hipMemcpyAsync(d_n, &mine, 8, hipMemcpyHostToDevice, b.s) != hipSuccess)
+            rc = set_error(FLRL_E_HIP, "flrl_fl_compress_rank: upload failed");
+        else if ((r1 = ncclAllReduce(d_n, d_n + 1, 1, ncclUint64, ncclSum, c->dev[0].nccl, b.s)) != ncclSuccess)
+            rc = rccl_error(r1, "ncclAllReduce");
+        else if (hipMemcpyAsync(&total_n, d_n + 1, 8, hipMemcpyDeviceToHost, b.s) != hipSuccess ||
+                 hipStreamSynchronize(b.s) != hipSuccess)
+            rc = set_error(FLRL_E_HIP, "flrl_fl_compress_rank: size read-back failed");
+    }
+    // gather the payloads to rank 0 (the reference's rank-0 merge, fl_gpu.cu:144-238,
+    // without padding or broadcasting them to every rank)
+    uint8_t *d_all = nullptr;
+    const uint64_t F = rec[FLRL_SZ_F_TOTAL], V = rec[FLRL_SZ_V_TOTAL];
+    if (rc == FLRL_OK && c->rank == 0 && hipMalloc(&d_all, (F + V) ? F + V : 16) != hipSuccess)
+        rc = set_error(FLRL_E_NOMEM, "Cannot allocate memory (device)");
+    // an error on one rank leaves the others waiting in ncclRecv/ncclSend, as
+    // in the reference; the per-rank caller aborts the job on error
+    if (rc == FLRL_OK) {
+        std::lock_guard<std::mutex> g(c->mu);
+        ncclComm_t nc = c->dev[0].nccl;
+        ncclResult_t r1 = ncclGroupStart();
+        if (c->rank == 0) {
+            uint64_t fo = 0, vo = 0;
+            for (size_t q = 0; q < R && r1 == ncclSuccess; ++q) {
+                const uint64_t fq = all[2 * q], vq = all[2 * q + 1];
+                if (q == 0) {
+                    if ((fq && hipMemcpyAsync(d_all, b.bits, fq, hipMemcpyDeviceToDevice, b.s) != hipSuccess) ||
+                        (vq && hipMemcpyAsync(d_all + F, b.vals, vq, hipMemcpyDeviceToDevice, b.s) != hipSuccess))
+                        r1 = ncclUnhandledCudaError;
+                } else {
+                    if (fq)
+                        r1 = ncclRecv(d_all + fo, fq, ncclUint8, (int)q, nc, b.s);
+                    if (r1 == ncclSuccess && vq)
+                        r1 = ncclRecv(d_all + F + vo, vq, ncclUint8, (int)q, nc, b.s);
+                }
+                fo += fq;
+                vo += vq;
+            }
+        } else {
+            if (rec[FLRL_SZ_F])
+                r1 = ncclSend(b.bits, rec[FLRL_SZ_F], ncclUint8, 0, nc, b.s);
+            if (r1 == ncclSuccess && rec[FLRL_SZ_V])
+                r1 = ncclSend(b.vals, rec[FLRL_SZ_V], ncclUint8, 0, nc, b.s);
+        }
+        const ncclResult_t r2 = ncclGroupEnd();
+        if (r1 != ncclSuccess || r2 != ncclSuccess)
+            rc = rccl_error(r1 != ncclSuccess ? r1 : r2, "flrl_fl_compress_rank: payload gather");
+        else if (hipStreamSynchronize(b.s) != hipSuccess)
+            rc = set_error(FLRL_E_HIP, "flrl_fl_compress_rank: stream failed");
+    }
+    if (rc == FLRL_OK && c->rank == 0) {
+        uint8_t *h_bits = static_cast<uint8_t *>(malloc(F ? F : 1));
+        uint8_t *h_vals = static_cast<uint8_t *>(malloc(V ? V : 1));
+        if (!h_bits || !h_vals ||
+            (F && hipMemcpy(h_bits, d_all, F, hipMemcpyDeviceToHost) != hipSuccess) ||
+            (V && hipMemcpy(h_vals, d_all + F, V, hipMemcpyDeviceToHost) != hipSuccess)) {
+            free(h_bits);
+            free(h_vals);
+            rc = set_error(FLRL_E_HIP, "flrl_fl_compress_rank: copy-out failed");
+        } else {
+            out->bits = h_bits;
+            out->bits_size = F;
+            out->values = h_vals;
+            out->values_size = V;
+            out->input_size = total_n;
+        }
+    }
+    if (d_all) {
+        (void)hipSetDevice(b.dev);
+        (void)hipStreamSynchronize(b.s);
+        (void)hipFree(d_all);
+    }
+    (void)hipSetDevice(prev);
+    return rc;
 }

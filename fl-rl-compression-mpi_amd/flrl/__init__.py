@@ -10,7 +10,10 @@ Host-buffer API (mirrors the reference's FixedLength::gpuCompress /
 gpuDecompress, src/fl/fl_gpu.cuh:14-15):
     fl_compress(data) -> FLCompressed(bits, values, input_size)
     fl_decompress(input_size, bits, values) -> np.ndarray[uint8]
-    fl_compress_sharded(data, ngpus) -> FLCompressed   (gpuNCCLCompress, :16)
+    fl_compress_sharded(data, nshards) -> FLCompressed (gpuNCCLCompress, :16)
+Multi-GPU (RCCL size exchange; gpuNCCLCompress, fl_gpu.cu:76-287):
+    Comm.local(ndev) / Comm.rank(nranks, comm_unique_id(), rank)
+    Comm.encode_rank / Comm.compress_rank / Comm.encode_sharded
     rl_compress(data) -> RLCompressed(counts, values, input_size)
     rl_decompress(input_size, counts, values) -> np.ndarray[uint8]
 Device API (raw device pointers as ints; mirrors gpuCompressDevice, :17):
@@ -116,6 +119,22 @@ _sig("flrl_rl_decode_scratch_bytes", _sz, _sz)
 _sig("flrl_rl_decode_device", ctypes.c_int, _vp, _vp, _sz, _vp, _sz, _vp, _sz, _vp)
 _sig("flrl_gen_device", ctypes.c_int, ctypes.c_int, _u64, _u64, _vp, _sz, _vp)
 _sig("flrl_gen_host", ctypes.c_int, ctypes.c_int, _u64, _u64, _vp, _sz)
+_pp = ctypes.POINTER(_vp)
+_sig("flrl_comm_init", ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int), _pp)
+_sig("flrl_comm_unique_id", ctypes.c_int, _vp)
+_sig("flrl_comm_init_rank", ctypes.c_int, ctypes.c_int, _vp, ctypes.c_int, _pp)
+_sig("flrl_comm_wrap", ctypes.c_int, _vp, _pp)
+_sig("flrl_comm_destroy", ctypes.c_int, _vp)
+_sig("flrl_comm_query", ctypes.c_int, _vp, ctypes.POINTER(ctypes.c_int),
+     ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int))
+_sig("flrl_fl_encode_rank", ctypes.c_int, _vp, _vp, _sz, _vp, _vp, _vp, _vp, _sz, _vp)
+_sig("flrl_fl_compress_rank", ctypes.c_int, _vp, _vp, _sz, ctypes.POINTER(_FLBuf))
+_sig("flrl_fl_encode_sharded", ctypes.c_int, _vp, ctypes.c_int, _pp, ctypes.POINTER(_sz), _pp, _pp,
+     _pp, _pp, ctypes.POINTER(_sz), _pp)
+
+UNIQUE_ID_BYTES = 128
+# per-shard sizes record written by the exchange (include/flrl.h FLRL_SZ_*)
+SZ_F, SZ_V, SZ_F_OFF, SZ_V_OFF, SZ_F_TOTAL, SZ_V_TOTAL, SZ_COUNT = range(7)
 
 _libc = ctypes.CDLL(None)
 _libc.free.argtypes = [_vp]
@@ -188,13 +207,97 @@ def fl_compress(data) -> FLCompressed:
                         int(buf.input_size))
 
 
-def fl_compress_sharded(data, ngpus: int = 0) -> FLCompressed:
+def fl_compress_sharded(data, nshards: int = 0) -> FLCompressed:
+    """Whole input in `nshards` shards (<= 0: one per GPU); shard r on GPU r mod ndev."""
     a = _as_u8(data)
     buf = _FLBuf()
-    _check(_lib.flrl_fl_compress_sharded(a.ctypes.data if a.size else None, a.size, ngpus,
+    _check(_lib.flrl_fl_compress_sharded(a.ctypes.data if a.size else None, a.size, nshards,
                                          ctypes.byref(buf)))
     return FLCompressed(_take(buf.bits, buf.bits_size), _take(buf.values, buf.values_size),
                         int(buf.input_size))
+
+
+def comm_unique_id() -> bytes:
+    """ncclGetUniqueId as FLRL_UNIQUE_ID_BYTES bytes (rank 0 distributes it)."""
+    b = ctypes.create_string_buffer(UNIQUE_ID_BYTES)
+    _check(_lib.flrl_comm_unique_id(b))
+    return b.raw
+
+
+class Comm:
+    """flrl_comm: an RCCL communicator for the FL size exchange, created once.
+
+    Comm.local(ndev)            one process driving ndev GPUs (ncclCommInitAll)
+    Comm.rank(nranks, uid, r)   one process per GPU (ncclCommInitRank, current device)
+    """
+
+    def __init__(self, handle: int):
+        self._h = handle
+
+    @classmethod
+    def local(cls, ndev: int = 0, devs=None) -> "Comm":
+        h = _vp()
+        arr = (ctypes.c_int * len(devs))(*devs) if devs else None
+        _check(_lib.flrl_comm_init(len(devs) if devs else ndev, arr, ctypes.byref(h)))
+        return cls(h.value)
+
+    @classmethod
+    def rank(cls, nranks: int, uid: bytes, rank: int) -> "Comm":
+        if len(uid) != UNIQUE_ID_BYTES:
+            raise ValueError(f"unique id must be {UNIQUE_ID_BYTES} bytes")
+        h = _vp()
+        _check(_lib.flrl_comm_init_rank(nranks, uid, rank, ctypes.byref(h)))
+        return cls(h.value)
+
+    @property
+    def handle(self) -> int:
+        if not self._h:
+            raise ValueError("communicator destroyed")
+        return self._h
+
+    def query(self) -> tuple[int, int, int]:
+        """(nranks, rank, local devices)."""
+        a, b, c = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        _check(_lib.flrl_comm_query(self.handle, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)))
+        return a.value, b.value, c.value
+
+    def encode_rank(self, d_in: int, n: int, d_bits: int, d_values: int, d_sizes: int,
+                    d_scratch: int, scratch_bytes: int, stream: int = 0) -> None:
+        _check(_lib.flrl_fl_encode_rank(self.handle, d_in, n, d_bits, d_values, d_sizes,
+                                        d_scratch, scratch_bytes, stream or None))
+
+    def compress_rank(self, data) -> FLCompressed:
+        """gpuNCCLCompress twin: this rank's shard in, merged result on rank 0."""
+        a = _as_u8(data)
+        buf = _FLBuf()
+        _check(_lib.flrl_fl_compress_rank(self.handle, a.ctypes.data if a.size else None, a.size,
+                                          ctypes.byref(buf)))
+        return FLCompressed(_take(buf.bits, buf.bits_size), _take(buf.values, buf.values_size),
+                            int(buf.input_size))
+
+    def encode_sharded(self, d_in, n, d_bits, d_values, d_sizes, d_scratch, scratch_bytes,
+                       streams) -> None:
+        P = len(d_in)
+        if not all(len(x) == P for x in (n, d_bits, d_values, d_sizes, d_scratch, scratch_bytes,
+                                         streams)):
+            raise ValueError("encode_sharded: per-shard lists differ in length")
+
+        def ptrs(xs):
+            return (_vp * P)(*[x or None for x in xs])
+        _check(_lib.flrl_fl_encode_sharded(self.handle, P, ptrs(d_in), (_sz * P)(*n), ptrs(d_bits),
+                                           ptrs(d_values), ptrs(d_sizes), ptrs(d_scratch),
+                                           (_sz * P)(*scratch_bytes), ptrs(streams)))
+
+    def destroy(self) -> None:
+        if self._h:
+            _lib.flrl_comm_destroy(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.destroy()
 
 
 def fl_compress_file(in_path: str, out_path: str, workers: int = 1, chunk_bytes: int = 0) -> None:

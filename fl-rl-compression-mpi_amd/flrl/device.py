@@ -52,6 +52,18 @@ class FLDevice:
                               self.sizes.data_ptr() + 8, self.scratch.data_ptr(),
                               self.scratch_bytes, _stream_handle(stream))
 
+    def encode_rank(self, comm: "flrl.Comm", x: torch.Tensor,
+                    stream: torch.cuda.Stream | None = None) -> None:
+        """Encode this rank's shard and run the size exchange (flrl_fl_encode_rank):
+        self.rank_sizes (int64[FLRL_SZ_COUNT], device) then holds this shard's
+        F, V, F_off, V_off and the totals, with no host round trip."""
+        _check_input(x, self.n)
+        if not hasattr(self, "rank_sizes"):
+            self.rank_sizes = torch.zeros(8, dtype=torch.int64, device=self.bits.device)
+        comm.encode_rank(x.data_ptr(), self.n, self.bits.data_ptr(), self.values.data_ptr(),
+                         self.rank_sizes.data_ptr(), self.scratch.data_ptr(), self.scratch_bytes,
+                         _stream_handle(stream))
+
     def decode(self, values_size: int, bits: torch.Tensor | None = None,
                values: torch.Tensor | None = None, out: torch.Tensor | None = None,
                stream: torch.cuda.Stream | None = None) -> torch.Tensor:

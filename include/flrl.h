@@ -81,13 +81,76 @@ int flrl_fl_decompress(size_t output_size, const uint8_t *bits, size_t bits_size
                        const uint8_t *values, size_t values_size,
                        uint8_t **out, size_t *out_size);
 
-/* Sharded encode across `ngpus` GPUs of this node (<= 0: all visible), one
- * process. Replaces FixedLength::gpuNCCLCompress (src/fl/fl_gpu.cuh:16,
- * fl_gpu.cu:76-287) and gpuMPICompress (fl_gpu.cuh:13, fl_gpu.cu:41-74):
- * 128-aligned shards by the reference rule (file_io.cu:46-51, size_t here),
- * one RCCL AllGather of {F_r, V_r} + exclusive scan to place the outputs. The
- * result is byte-identical to flrl_fl_compress. */
-int flrl_fl_compress_sharded(const uint8_t *data, size_t size, int ngpus, flrl_fl_buf *out);
+/* Sharded encode of a host buffer in `nshards` 128-aligned shards (<= 0: one
+ * per visible GPU), one process; shard r runs on device r mod ndev, ndev =
+ * min(nshards, visible devices), so any shard count runs on any node.
+ * Replaces FixedLength::gpuNCCLCompress (src/fl/fl_gpu.cuh:16,
+ * fl_gpu.cu:76-287) and gpuMPICompress (fl_gpu.cuh:13, fl_gpu.cu:41-74) for a
+ * caller holding the whole input: shards by the reference rule
+ * (file_io.cu:46-51, size_t here), flrl_fl_encode_sharded on a communicator
+ * cached per device count (created once per process, not per call). The result
+ * is byte-identical to flrl_fl_compress. */
+int flrl_fl_compress_sharded(const uint8_t *data, size_t size, int nshards, flrl_fl_buf *out);
+
+/* ---- FL, multi-GPU: communicators and the size exchange -------------------
+ * The only collective on the data path is one RCCL all-gather of {F_r, V_r}
+ * (16 B per shard over xGMI) followed by an exclusive scan on the device; every
+ * shard learns where its bits/values go in the whole-input output. A comm is
+ * created once and reused (ncclCommInitAll/InitRank cost ~100 ms). */
+typedef struct flrl_comm flrl_comm;
+#define FLRL_UNIQUE_ID_BYTES 128 /* sizeof(ncclUniqueId) */
+
+/* Per-shard sizes record (device u64[FLRL_SZ_COUNT]) the exchange writes. */
+enum {
+    FLRL_SZ_F = 0,       /* this shard's bitsSize  (= ceil(n_r/128)) */
+    FLRL_SZ_V = 1,       /* this shard's valuesSize */
+    FLRL_SZ_F_OFF = 2,   /* byte offset of its bits in the whole output */
+    FLRL_SZ_V_OFF = 3,   /* byte offset of its values in the whole output */
+    FLRL_SZ_F_TOTAL = 4, /* whole-input bitsSize */
+    FLRL_SZ_V_TOTAL = 5, /* whole-input valuesSize */
+    FLRL_SZ_COUNT = 6
+};
+
+/* One process driving `ndev` GPUs of this node (devs NULL: 0..ndev-1; ndev <= 0:
+ * all visible); ncclCommInitAll. */
+int flrl_comm_init(int ndev, const int *devs, flrl_comm **out);
+/* One process per GPU (the reference's MPI model, main.cu:46-70): rank 0 calls
+ * flrl_comm_unique_id and distributes the FLRL_UNIQUE_ID_BYTES bytes (MPI_Bcast,
+ * torch.distributed, a file ...); every rank calls flrl_comm_init_rank with the
+ * current HIP device set to its GPU (ncclCommInitRank). */
+int flrl_comm_unique_id(void *id);
+int flrl_comm_init_rank(int nranks, const void *id, int rank, flrl_comm **out);
+/* Wrap an existing ncclComm_t (e.g. MpiNcclData::ncclComm, mpi_common.cuh);
+ * not destroyed by flrl_comm_destroy. */
+int flrl_comm_wrap(void *nccl_comm, flrl_comm **out);
+int flrl_comm_destroy(flrl_comm *c);
+int flrl_comm_query(const flrl_comm *c, int *nranks, int *rank, int *ndev);
+
+/* Per-rank device-resident encode + exchange (per-rank comm): encodes this
+ * rank's shard like flrl_fl_encode_device, then fills d_sizes
+ * (u64[FLRL_SZ_COUNT], device) with its sizes, offsets and the totals, all on
+ * `stream` with no host synchronisation. Every rank of the comm must call it
+ * (collective). The device half of gpuNCCLCompress (fl_gpu.cu:76-143). */
+int flrl_fl_encode_rank(flrl_comm *c, const uint8_t *d_in, size_t n, uint8_t *d_bits,
+                        uint8_t *d_values, uint64_t *d_sizes, void *d_scratch,
+                        size_t scratch_bytes, void *stream);
+
+/* Host-buffer per-rank twin of gpuNCCLCompress(data, size, MpiNcclData)
+ * (fl_gpu.cuh:16): each rank passes its own shard (loadFileMpi, file_io.cu:28-71);
+ * rank 0 receives the merged whole-input result (input_size = sum of the
+ * ranks' sizes), the other ranks an empty flrl_fl_buf — the reference's rank-0
+ * merge (fl_gpu.cu:196-238). Payloads travel ncclSend/ncclRecv to rank 0 only. */
+int flrl_fl_compress_rank(flrl_comm *c, const uint8_t *data, size_t size, flrl_fl_buf *out);
+
+/* Single-process device-resident sharded encode (flrl_comm_init comm): shard r
+ * (d_in[r], n[r]; all but the last a multiple of 128 bytes) with its buffers on
+ * device devs[r mod ndev], encoded on streams[r]; after the call every
+ * streams[r] is ordered after the exchange, and d_sizes[r] holds shard r's
+ * record. At most 64 shards per device. */
+int flrl_fl_encode_sharded(flrl_comm *c, int nshards, const uint8_t *const *d_in, const size_t *n,
+                           uint8_t *const *d_bits, uint8_t *const *d_values,
+                           uint64_t *const *d_sizes, void *const *d_scratch,
+                           const size_t *scratch_bytes, void *const *streams);
 
 /* ---- FL, file to file, streamed through GPUs ---
  * The CLI's `c|d fl` (workers = 1) and `fl-mpi` / `fl-nccl` / `fl-shmem`

@@ -1,0 +1,44 @@
+"""bench.py's rank launcher (CPU): `python bench.py --gpus N` with N > 1 and no
+torch.distributed environment starts the N ranks itself, as a child
+torch.distributed.run (never an exec), before anything touches the GPU."""
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import bench  # noqa: E402
+
+
+def test_single_gpu_runs_in_process():
+    assert bench.rank_launch_cmd([], {}) is None
+    assert bench.rank_launch_cmd(["--gpus", "1", "--steps", "3"], {}) is None
+
+
+def test_already_a_rank_does_not_relaunch():
+    env = {"WORLD_SIZE": "8", "RANK": "3", "LOCAL_RANK": "3"}
+    assert bench.rank_launch_cmd(["--gpus", "8"], env) is None
+
+
+def test_launch_command_shape():
+    argv = ["--gpus", "8", "--steps", "7", "--warmup", "2"]
+    cmd = bench.rank_launch_cmd(argv, {})
+    assert cmd[:3] == [sys.executable, "-m", "torch.distributed.run"]
+    assert "--nproc-per-node=8" in cmd and "--nnodes=1" in cmd
+    assert "--master-addr=127.0.0.1" in cmd
+    port = [c for c in cmd if c.startswith("--master-port=")]
+    assert len(port) == 1 and 0 < int(port[0].split("=")[1]) < 65536
+    i = cmd.index(os.path.join(ROOT, "bench.py"))
+    assert cmd[i + 1:] == argv  # the ranks see the same arguments
+    assert bench.rank_launch_cmd(["--gpus=4"], {})[4] == "--nproc-per-node=4"
+
+
+def test_launcher_end_to_end_help():
+    """The parent spawns 2 ranks that parse their own arguments (--help exits
+    before any device work) and returns their exit status."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--help"],
+                       capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert r.stdout.count("usage:") == 2  # each rank printed its usage

@@ -283,17 +283,6 @@ def test_device_repeat_stability(kind):
     torch.cuda.empty_cache()
 
 
-# ------------------------------------------------------------------ sharded
-def test_sharded_equals_single(bmp_bytes):
-    ng = flrl.device_count()
-    c1 = flrl.fl_compress(bmp_bytes)
-    for p in range(1, ng + 1):
-        cp = flrl.fl_compress_sharded(bmp_bytes, p)
-        assert np.array_equal(cp.bits, c1.bits) and np.array_equal(cp.values, c1.values)
-    with pytest.raises(flrl.FLRLError):
-        flrl.fl_compress_sharded(bmp_bytes, ng + 1)
-
-
 # ---------------------------------------------------------------------- CLI
 def test_cli_gpu_methods(golden, bmp_bytes, cli_path, tmp_path):
     src = tmp_path / "in.bmp"
