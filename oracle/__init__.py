@@ -42,6 +42,14 @@ _lib.orc_rl_compress.restype = _sz
 _lib.orc_rl_compress.argtypes = [_vp, _sz, _vp, _vp]
 _lib.orc_rl_decompress.restype = _sz
 _lib.orc_rl_decompress.argtypes = [_vp, _vp, _sz, _vp, _sz]
+_lib.orc_fl_widths_frame.restype = _sz
+_lib.orc_fl_widths_frame.argtypes = [_vp, _sz, _sz, _vp]
+_lib.orc_fl_frame_starts.restype = None
+_lib.orc_fl_frame_starts.argtypes = [_vp, _sz, _sz, _vp]
+_lib.orc_fl_compress_frame.restype = _sz
+_lib.orc_fl_compress_frame.argtypes = [_vp, _sz, _sz, _vp, _vp]
+_lib.orc_fl_decompress_frame.restype = _sz
+_lib.orc_fl_decompress_frame.argtypes = [_sz, _sz, _vp, _sz, _vp, _sz, _vp]
 _lib.orc_gen.restype = ctypes.c_int
 _lib.orc_gen.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64, _vp, _sz]
 _lib.orc_clz8.restype = ctypes.c_uint8
@@ -73,6 +81,38 @@ def fl_compress(data) -> tuple[np.ndarray, np.ndarray]:
     values = np.zeros(max(n, 1), dtype=np.uint8)
     v = _lib.orc_fl_compress(_ptr(a), n, _ptr(bits), values.ctypes.data)
     return bits, values[:v].copy()
+
+
+def fl_widths_frame(data, frame_len: int) -> tuple[np.ndarray, np.ndarray, int]:
+    """Width pass + frameStartIndices at any frame length (IMPLEMENTATION-PLAN.md:9-29)
+    -> (bits, starts, total_bits)."""
+    a = np.ascontiguousarray(data, dtype=np.uint8).reshape(-1)
+    frames = (a.size + frame_len - 1) // frame_len
+    bits = np.zeros(max(frames, 1), dtype=np.uint8)
+    total = _lib.orc_fl_widths_frame(_ptr(a), a.size, frame_len, bits.ctypes.data)
+    starts = np.zeros(max(frames, 1), dtype=np.uint64)
+    _lib.orc_fl_frame_starts(bits.ctypes.data, frames, frame_len, starts.ctypes.data)
+    return bits[:frames].copy(), starts[:frames].copy(), int(total)
+
+
+def fl_compress_frame(data, frame_len: int) -> tuple[np.ndarray, np.ndarray]:
+    """cpuCompress at any frame length -> (bits, values)."""
+    a = np.ascontiguousarray(data, dtype=np.uint8).reshape(-1)
+    frames = (a.size + frame_len - 1) // frame_len
+    bits = np.zeros(max(frames, 1), dtype=np.uint8)
+    values = np.zeros(max(a.size, 1), dtype=np.uint8)
+    v = _lib.orc_fl_compress_frame(_ptr(a), a.size, frame_len, bits.ctypes.data, values.ctypes.data)
+    return bits[:frames].copy(), values[:v].copy()
+
+
+def fl_decompress_frame(output_size: int, frame_len: int, bits, values) -> np.ndarray:
+    """cpuDecompress at any frame length."""
+    bits = np.ascontiguousarray(bits, dtype=np.uint8)
+    values = np.ascontiguousarray(values, dtype=np.uint8)
+    out = np.zeros(max(output_size, 1), dtype=np.uint8)
+    got = _lib.orc_fl_decompress_frame(output_size, frame_len, _ptr(bits), bits.size, _ptr(values),
+                                       values.size, out.ctypes.data)
+    return out[:got].copy()
 
 
 def fl_decompress(output_size: int, bits: np.ndarray, values: np.ndarray) -> np.ndarray:

@@ -35,27 +35,47 @@ size_t orc_fl_frames(size_t n) { return (n + ORC_FRAME_LENGTH - 1) / ORC_FRAME_L
 
 size_t orc_fl_values_bound(size_t n) { return n; }
 
-size_t orc_fl_compress(const uint8_t *data, size_t n, uint8_t *bits, uint8_t *values)
+/* The restatement is written for any frame length L (the reference fixes
+ * L = FRAME_LENGTH = 128, fl_common.cuh:9; IMPLEMENTATION-PLAN.md:9-27 works its
+ * example at L = 3), so the plan's worked example can pin it. */
+size_t orc_fl_widths_frame(const uint8_t *data, size_t n, size_t frame_len, uint8_t *bits)
 {
-    if (n == 0) /* fl_cpu.cu:11-14 */
-        return 0;
-    const size_t frames = orc_fl_frames(n);
-
     /* width pass, fl_cpu.cu:35-50: b_f = max(1, max_i (8 - clz8(x_i))) */
+    const size_t frames = (n + frame_len - 1) / frame_len;
     size_t total_bits = 0;
     for (size_t f = 0; f < frames; f++) {
         uint8_t min_bits = 1;
-        for (size_t i = 0; i < ORC_FRAME_LENGTH && f * ORC_FRAME_LENGTH + i < n; i++) {
-            uint8_t required = (uint8_t)(8 - orc_clz8(data[f * ORC_FRAME_LENGTH + i]));
+        for (size_t i = 0; i < frame_len && f * frame_len + i < n; i++) {
+            uint8_t required = (uint8_t)(8 - orc_clz8(data[f * frame_len + i]));
             if (required > min_bits)
                 min_bits = required;
         }
         bits[f] = min_bits;
-        size_t cnt = n - ORC_FRAME_LENGTH * f;
-        if (cnt > ORC_FRAME_LENGTH)
-            cnt = ORC_FRAME_LENGTH;
+        size_t cnt = n - frame_len * f;
+        if (cnt > frame_len)
+            cnt = frame_len;
         total_bits += (size_t)min_bits * cnt;
     }
+    return total_bits;
+}
+
+void orc_fl_frame_starts(const uint8_t *bits, size_t frames, size_t frame_len, uint64_t *starts)
+{
+    /* frameStartIndices = Prescan(bits[f] * frame_len), IMPLEMENTATION-PLAN.md:20-29 */
+    uint64_t acc = 0;
+    for (size_t f = 0; f < frames; f++) {
+        starts[f] = acc;
+        acc += (uint64_t)bits[f] * frame_len;
+    }
+}
+
+size_t orc_fl_compress_frame(const uint8_t *data, size_t n, size_t frame_len, uint8_t *bits,
+                             uint8_t *values)
+{
+    if (n == 0 || frame_len == 0) /* fl_cpu.cu:11-14 */
+        return 0;
+    const size_t frames = (n + frame_len - 1) / frame_len;
+    const size_t total_bits = orc_fl_widths_frame(data, n, frame_len, bits);
 
     /* valuesSize = ceil(totalBits/8), zero-filled, fl_cpu.cu:53-55 */
     const size_t values_size = (total_bits + 7) / 8;
@@ -65,8 +85,8 @@ size_t orc_fl_compress(const uint8_t *data, size_t n, uint8_t *bits, uint8_t *va
     size_t used = 0;
     for (size_t f = 0; f < frames; f++) {
         const uint8_t b = bits[f];
-        for (size_t i = 0; i < ORC_FRAME_LENGTH && f * ORC_FRAME_LENGTH + i < n; i++) {
-            const uint8_t v = data[f * ORC_FRAME_LENGTH + i];
+        for (size_t i = 0; i < frame_len && f * frame_len + i < n; i++) {
+            const uint8_t v = data[f * frame_len + i];
             const size_t id = used / 8;
             const uint8_t off = (uint8_t)(used % 8);
             values[id] |= (uint8_t)(v << off);
@@ -78,15 +98,21 @@ size_t orc_fl_compress(const uint8_t *data, size_t n, uint8_t *bits, uint8_t *va
     return values_size;
 }
 
-size_t orc_fl_decompress(size_t output_size, const uint8_t *bits, size_t bits_size,
-                         const uint8_t *values, size_t values_size, uint8_t *out)
+size_t orc_fl_compress(const uint8_t *data, size_t n, uint8_t *bits, uint8_t *values)
 {
-    if (values_size == 0 || bits_size == 0) /* fl_cpu.cu:94-97 */
+    return orc_fl_compress_frame(data, n, ORC_FRAME_LENGTH, bits, values);
+}
+
+size_t orc_fl_decompress_frame(size_t output_size, size_t frame_len, const uint8_t *bits,
+                               size_t bits_size, const uint8_t *values, size_t values_size,
+                               uint8_t *out)
+{
+    if (values_size == 0 || bits_size == 0 || frame_len == 0) /* fl_cpu.cu:94-97 */
         return 0;
     size_t consumed = 0;
     for (size_t f = 0; f < bits_size; f++) { /* fl_cpu.cu:117-141 */
         const uint8_t b = bits[f];
-        for (size_t i = 0; i < ORC_FRAME_LENGTH && f * ORC_FRAME_LENGTH + i < output_size; i++) {
+        for (size_t i = 0; i < frame_len && f * frame_len + i < output_size; i++) {
             const size_t id = consumed / 8;
             const uint8_t off = (uint8_t)(consumed % 8);
             const uint8_t mask = (uint8_t)((1u << b) - 1);
@@ -96,11 +122,18 @@ size_t orc_fl_decompress(size_t output_size, const uint8_t *bits, size_t bits_si
                 const uint8_t om = (uint8_t)((1u << ob) - 1);
                 v |= (uint8_t)((values[id + 1] & om) << (b - ob));
             }
-            out[f * ORC_FRAME_LENGTH + i] = v;
+            out[f * frame_len + i] = v;
             consumed += b;
         }
     }
     return output_size;
+}
+
+size_t orc_fl_decompress(size_t output_size, const uint8_t *bits, size_t bits_size,
+                         const uint8_t *values, size_t values_size, uint8_t *out)
+{
+    return orc_fl_decompress_frame(output_size, ORC_FRAME_LENGTH, bits, bits_size, values,
+                                   values_size, out);
 }
 
 size_t orc_rl_compress(const uint8_t *data, size_t n, uint8_t *counts, uint8_t *values)

@@ -46,6 +46,18 @@ size_t orc_fl_compress(const uint8_t *data, size_t n, uint8_t *bits, uint8_t *va
 size_t orc_fl_decompress(size_t output_size, const uint8_t *bits, size_t bits_size,
                          const uint8_t *values, size_t values_size, uint8_t *out);
 
+/* The same two passes at any frame length (the reference fixes 128; the plan's
+ * worked example, IMPLEMENTATION-PLAN.md:9-27, uses 3). Widths: bits[f] for
+ * ceil(n/frame_len) frames, returns the total bit count. Starts: the plan's
+ * frameStartIndices (bit offset of each frame, exclusive scan of b_f*frame_len). */
+size_t orc_fl_widths_frame(const uint8_t *data, size_t n, size_t frame_len, uint8_t *bits);
+void orc_fl_frame_starts(const uint8_t *bits, size_t frames, size_t frame_len, uint64_t *starts);
+size_t orc_fl_compress_frame(const uint8_t *data, size_t n, size_t frame_len, uint8_t *bits,
+                             uint8_t *values);
+size_t orc_fl_decompress_frame(size_t output_size, size_t frame_len, const uint8_t *bits,
+                               size_t bits_size, const uint8_t *values, size_t values_size,
+                               uint8_t *out);
+
 /* RL encode, IMPLEMENTATION-PLAN.md:85-152: maximal runs of equal bytes, runs
  * longer than 255 split into 255-chunks counted from the run start (:125).
  * counts/values must hold n bytes. Returns the number of runs R. */

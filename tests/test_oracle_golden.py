@@ -35,6 +35,45 @@ def test_fl_kats(golden):
         assert back.tobytes() == data
 
 
+def test_fl_plan_example_frame3():
+    """The one reference-held FL vector (IMPLEMENTATION-PLAN.md:9-27): at frame
+    length 3, input [0,2,1,5,5,7,10,1,13] has outputBits [2,3,4] and
+    frameStartIndices [0,6,15]; outputValues is ceil((15 + 3*4)/8) = 4 bytes
+    whose fields, read at bitsOffset = start[f] + k*b (plan :35-40), are the
+    plan's binary strings 00_10_01---101_101_111---1010_0001_1101."""
+    data = np.array([0, 2, 1, 5, 5, 7, 10, 1, 13], np.uint8)
+    bits, starts, total = oracle.fl_widths_frame(data, 3)
+    assert bits.tolist() == [2, 3, 4]
+    assert starts.tolist() == [0, 6, 15]
+    assert total == 27
+    b2, values = oracle.fl_compress_frame(data, 3)
+    assert b2.tolist() == [2, 3, 4] and values.size == 4
+    stream = int.from_bytes(values.tobytes(), "little")
+    fields = []
+    for i in range(data.size):
+        f, k = divmod(i, 3)
+        off = int(starts[f]) + k * int(bits[f])
+        fields.append(format((stream >> off) & ((1 << int(bits[f])) - 1), f"0{bits[f]}b"))
+    rendered = "---".join("_".join(fields[3 * f:3 * f + 3]) for f in range(3))
+    assert rendered == "00_10_01---101_101_111---1010_0001_1101"
+    assert oracle.fl_decompress_frame(data.size, 3, bits, values).tolist() == data.tolist()
+    # at the reference's frame length the same input is one frame of width 4
+    b128, _ = oracle.fl_compress(data)
+    assert b128.tolist() == [4]
+
+
+def test_fl_frame_length_generic_matches_128():
+    """orc_fl_compress is the frame-length-generic restatement at 128."""
+    a = oracle.gen("lo4", 100_003, 9)
+    a[::997] = 0xFF
+    bits, values = oracle.fl_compress(a)
+    b2, v2 = oracle.fl_compress_frame(a, 128)
+    assert np.array_equal(bits, b2) and np.array_equal(values, v2)
+    for L in (1, 3, 7, 200):
+        b, v = oracle.fl_compress_frame(a, L)
+        assert np.array_equal(oracle.fl_decompress_frame(a.size, L, b, v), a)
+
+
 def test_fl_empty_file(golden):
     blob = oracle.fl_file_bytes(np.zeros(0, np.uint8))
     assert blob == bytes(24)
