@@ -735,6 +735,372 @@ __global__ __launch_bounds__(T) void rl_encode_kernel(
     }
 }
 
+// Wave-private variant. The tile is the same 128 KiB, but wave w owns its w-th
+// contiguous 32 KiB chunk and streams it as SUB sub-chunks of 8 KiB through its
+// OWN 8 KiB of LDS (registers -> ds_write -> each lane reads its 128 contiguous
+// bytes; LDS ops of one wave are in order, so no barrier), with the next
+// sub-chunk's loads in flight during each scan. All scans are wave scans with
+// the carries (PhaseMap, first natural head, state-independent head count) in
+// uniform registers, and each wave stages its own state-independent runs, so a
+// tile has three block barriers (ticket, wave maps, state) instead of four per
+// sub-tile. The wave maps compose (sm_compose) into the tile's map for the one
+// look-back; the resolved state is then advanced wave by wave, and every wave
+// emits its own prefix (split heads before its first natural head), staged runs
+// and, past a staging overflow, re-read sub-chunks (as rl_encode_kernel).
+template <int T, int LB, int SUB>
+__global__ __launch_bounds__(T) void rl_encode_wave_kernel(
+    const uint8_t *__restrict__ in, uint64_t n, uint32_t ntiles, uint8_t *__restrict__ counts,
+    uint8_t *__restrict__ values, uint64_t *__restrict__ runs_out, Ctrl *ctrl, uint64_t *status)
+{
+    constexpr int W = T / kWave;
+    constexpr int CH = LB / 16;      // 16-byte chunks per lane
+    constexpr int WB = kWave * LB;   // sub-chunk bytes
+    constexpr int CB = WB * SUB;     // wave chunk bytes
+    constexpr int TBT = CB * W;      // tile bytes
+    constexpr int SW = kRlStageBytes / W / 2;  // staged records per wave
+    constexpr int NJ = WB / 1024;    // 1 KiB wave-loads per sub-chunk
+    constexpr uint32_t kNone = 0xFFFFFFFFu;
+    static_assert(LB == 128, "the swizzle and the 2 x u64 head masks assume 8 chunks per lane");
+    static_assert(TBT == kRlTileBytes, "tile geometry shared with the layout");
+    __shared__ __attribute__((aligned(16))) uint8_t s_lds[W * WB + kRlStageBytes];
+    __shared__ uint64_t s_map[W];
+    __shared__ uint64_t s_st[W];
+    __shared__ uint32_t s_ticket;
+
+    const int tid = threadIdx.x;
+    const int lane = tid & (kWave - 1);
+    const int w = tid / kWave;
+    uint8_t *const img = s_lds + w * WB;
+    uint8_t *const stc = s_lds + W * WB + w * 2 * SW;
+    uint8_t *const stv = stc + SW;
+    const uint32_t row = (uint32_t)lane;
+    const uint32_t o = row * LB;
+    const uint8_t *my = img + o;
+
+    const uint32_t tile = take_ticket(ctrl, &s_ticket);
+    if (tile >= ntiles) {  // the scratch's ticket was not reset for this launch
+        if (threadIdx.x == 0)
+            raise_error(ctrl, FLRL_E_ARG);
+        return;
+    }
+    const uint64_t chunk_off = (uint64_t)tile * TBT + (uint64_t)w * CB;
+    const uint32_t chunk_len = chunk_off >= n ? 0u : (n - chunk_off < (uint64_t)CB ? (uint32_t)(n - chunk_off) : (uint32_t)CB);
+    const int ns = (int)((chunk_len + WB - 1) / WB);  // sub-chunks of this wave
+    const uint32_t swz_c = ((uint32_t)lane & 7u) ^ (((uint32_t)lane >> 3) & 7u);
+
+    // sub-chunk s into registers, placed as the LDS image wants it: row r keeps
+    // chunk c at r*LB + ((c ^ (r & 7)) * 16), each wave-load 1 KiB contiguous
+    auto load_sub = [&](int s, u32x4 (&pf)[NJ]) {
+        const uint64_t so = chunk_off + (uint64_t)s * WB;
+        if (so + WB <= n) {
+#pragma unroll
+            for (int j = 0; j < NJ; ++j)
+                pf[j] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(
+                    in + so + (uint32_t)(j * 8 + lane / 8) * LB + swz_c * 16));
+        } else {
+#pragma unroll
+            for (int j = 0; j < NJ; ++j)
+                pf[j] = load16_tail(in, so + (uint32_t)(j * 8 + lane / 8) * LB + swz_c * 16, n);
+        }
+    };
+    struct Sub {
+        uint32_t nat[CH / 2];  // 16-bit masks, two per word
+        uint32_t ncnt, fpos, lpos, vbl, p0;
+        uint32_t lrel;    // lane start state from the sub-chunk's start (PhaseMap)
+        uint32_t smap;    // the sub-chunk's PhaseMap
+        uint32_t sfirst;  // first natural head in the sub-chunk (kNone: none)
+    };
+    // sub-chunk s (in pf) through the wave's LDS image; p_sub = the byte before
+    // it; pf_next: load sub-chunk s+1 into pf once this one is in LDS. Returns
+    // the sub-chunk's last byte (uniform).
+    auto scan_sub = [&](int s, Sub &L, u32x4 (&pf)[NJ], uint32_t p_sub, bool pf_next) -> uint32_t {
+        const uint64_t so = chunk_off + (uint64_t)s * WB;
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+            *reinterpret_cast<u32x4 *>(img + j * 1024 + lane * 16) = pf[j];
+        if (pf_next)
+            load_sub(s + 1, pf);  // lands while this sub-chunk is scanned
+        const uint64_t lane_off = so + o;
+        L.vbl = lane_off >= n ? 0u : (n - lane_off >= LB ? (uint32_t)LB : (uint32_t)(n - lane_off));
+        u32x4 x[CH];
+#pragma unroll
+        for (int c = 0; c < CH; ++c)
+            x[c] = *reinterpret_cast<const u32x4 *>(my + ((c ^ (row & 7u)) * 16));
+        const uint32_t mylast = x[CH - 1].w >> 24;
+        const uint32_t up = (uint32_t)__shfl_up((int)mylast, 1, kWave);
+        L.p0 = lane == 0 ? p_sub : up;
+        {
+            uint32_t p = L.p0;
+            const bool full = so + WB <= n;  // wave-uniform: no per-chunk length masks
+#pragma unroll
+            for (int c = 0; c < CH; ++c) {
+                uint32_t m = nat_mask(x[c], p);
+                if (!full) {
+                    const uint32_t vb = L.vbl > 16u * c ? (L.vbl - 16u * c >= 16 ? 16u : L.vbl - 16u * c) : 0u;
+                    m &= vb >= 16 ? 0xFFFFu : ((1u << vb) - 1u);
+                }
+                if (c & 1)
+                    L.nat[c / 2] |= m << 16;
+                else
+                    L.nat[c / 2] = m;
+                p = x[c].w >> 24;
+            }
+            if (lane_off == 0)
+                L.nat[0] |= 1u;  // byte 0 is a head
+            const uint64_t a = ((uint64_t)L.nat[1] << 32) | L.nat[0], b = ((uint64_t)L.nat[3] << 32) | L.nat[2];
+            L.ncnt = (uint32_t)(__popcll(a) + __popcll(b));
+            L.fpos = a ? (uint32_t)__builtin_ctzll(a) : (b ? 64u + (uint32_t)__builtin_ctzll(b) : (uint32_t)LB);
+            L.lpos = b ? 127u - (uint32_t)__builtin_clzll(b) : (a ? 63u - (uint32_t)__builtin_clzll(a) : 0u);
+        }
+        const bool has = L.ncnt != 0;
+        const uint32_t lmap = has ? pm_make(true, L.vbl - L.lpos) : pm_make(false, L.vbl);
+        const uint32_t incl = wave_incl_scan_map(lmap);
+        uint32_t lexcl = __shfl_up(incl, 1, kWave);
+        L.lrel = lane == 0 ? kMapIdent : lexcl;
+        L.smap = (uint32_t)__builtin_amdgcn_readlane((int)incl, kWave - 1);
+        const unsigned long long hb = __ballot(has);
+        const int fl = hb ? __ffsll(hb) - 1 : 0;
+        const uint32_t ff = (uint32_t)__shfl(L.fpos, fl, kWave);
+        L.sfirst = hb ? (uint32_t)fl * LB + ff : kNone;
+        return (uint32_t)__builtin_amdgcn_readlane((int)mylast, kWave - 1);
+    };
+    auto head_masks = [&](const Sub &L, uint32_t c0, bool with_split, uint64_t &h0, uint64_t &h1) {
+        const uint32_t j0 = c0 == 0 ? 0u : 255u - c0;
+        const bool split = with_split && j0 < L.fpos && j0 < L.vbl;
+        h0 = h1 = 0;
+#pragma unroll
+        for (int c = 0; c < CH; ++c) {
+            uint32_t h = (L.nat[c / 2] >> (16 * (c & 1))) & 0xFFFFu;
+            if (split && (j0 >> 4) == (uint32_t)c)
+                h |= 1u << (j0 & 15u);
+            if (c < 4)
+                h0 |= (uint64_t)h << (16 * c);
+            else
+                h1 |= (uint64_t)h << (16 * (c - 4));
+        }
+    };
+    // a lane's runs from its head masks (see rl_encode_kernel::lane_runs)
+    auto lane_runs = [&](const Sub &L, uint64_t h0, uint64_t h1, uint32_t c_first, uint8_t *sc, uint8_t *sv,
+                         uint32_t slot) {
+        int prev = -1;
+        uint32_t val = L.p0;
+        while (h0 | h1) {
+            int pos;
+            if (h0) {
+                pos = __builtin_ctzll(h0);
+                h0 &= h0 - 1;
+            } else {
+                pos = 64 + __builtin_ctzll(h1);
+                h1 &= h1 - 1;
+            }
+            uint32_t cnt = prev < 0 ? add_c(c_first, (uint32_t)pos) : (uint32_t)(pos - prev);
+            cnt = cnt == 0 ? 255u : cnt;
+            const uint32_t q = (uint32_t)pos;
+            const uint32_t nval = my[(((q >> 4) ^ (row & 7u)) * 16) + (q & 15u)];
+            sc[slot] = (uint8_t)cnt;
+            sv[slot] = (uint8_t)val;
+            val = nval;
+            ++slot;
+            prev = pos;
+        }
+    };
+
+    // ---- this wave's chunk: stage the state-independent runs ----------------
+    u32x4 pf[NJ];
+    uint32_t p_sub = 0, v0 = 0;
+    if (ns > 0) {
+        load_sub(0, pf);
+        p_sub = chunk_off > 0 ? (uint32_t)in[chunk_off - 1] : 0u;
+    }
+    uint32_t rel_in = kMapIdent;   // PhaseMap from the chunk start to this sub-chunk
+    uint32_t first = kNone;        // the chunk's first natural head (chunk-relative)
+    uint32_t K = 0;                // state-independent heads so far
+    int nst = SUB;                 // sub-chunks whose runs are all staged
+    uint32_t Kst = 0, rel_st = kMapIdent;
+    for (int s = 0; s < ns; ++s) {
+        Sub L;
+        const uint32_t last = scan_sub(s, L, pf, p_sub, s + 1 < ns);
+        if (s == 0)
+            v0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)img[0]);
+        p_sub = last;
+        const bool seen = first != kNone;
+        const uint32_t lrel = pm_compose(rel_in, L.lrel);
+        bool lane_indep = false, after = false;
+        if (seen) {
+            lane_indep = after = true;
+        } else if (L.sfirst != kNone && o + LB > L.sfirst) {
+            lane_indep = true;
+            after = o > L.sfirst;
+        }
+        const uint32_t cr = after ? pm_apply(lrel, 1) : 0u;  // constant after the first head
+        uint64_t h0 = 0, h1 = 0;
+        uint32_t indep = 0;
+        if (lane_indep) {
+            head_masks(L, cr, after, h0, h1);
+            indep = (uint32_t)(__popcll(h0) + __popcll(h1));
+        }
+        const uint32_t hincl = wave_incl_scan_u32(indep);
+        const uint32_t ks = (uint32_t)__builtin_amdgcn_readlane((int)hincl, kWave - 1);
+        if (nst == SUB && K + ks > (uint32_t)SW) {  // wave-uniform
+            nst = s;
+            Kst = K;
+            rel_st = rel_in;
+        }
+        const uint32_t slot = K + (hincl - indep);
+        if (!seen && L.sfirst != kNone)
+            first = (uint32_t)s * WB + L.sfirst;
+        K += ks;
+        rel_in = pm_compose(rel_in, L.smap);
+        if (nst == SUB && indep)
+            lane_runs(L, h0, h1, cr, stc, stv, slot);
+    }
+    if (nst >= ns) {
+        nst = ns;
+        Kst = K;
+        rel_st = rel_in;
+    }
+    const uint32_t pre = first != kNone ? first : chunk_len;
+
+    // ---- the wave maps -> the tile's map -> ONE look-back -> each wave's state
+    if (lane == 0)
+        s_map[w] = first != kNone ? sm_nat(first, K, rel_in & 0xFFu) : sm_nonat(chunk_len);
+    __syncthreads();
+    if (w == 0) {
+        uint64_t tmap = s_map[0];
+#pragma unroll
+        for (int v = 1; v < W; ++v)
+            tmap = sm_compose(tmap, s_map[v]);
+        publish_seg(status, tile, tmap);
+        uint64_t st = lookback_seg<kRlLookG>(status, tile, tmap, ctrl);
+        if (lane == 0) {
+#pragma unroll
+            for (int v = 0; v < W; ++v) {
+                s_st[v] = st;
+                st = sm_compose(st, s_map[v]);
+            }
+        }
+    }
+    __syncthreads();
+    if (ns == 0)
+        return;
+    const uint64_t h_in = sm_h(s_st[w]);
+    const uint32_t c_in = sm_c(s_st[w]);
+    {
+        // staged sub-chunks [0, nst): split heads h_in + j end full 255-byte
+        // chunks of the chunk's first byte, then the staged records
+        const uint32_t st_len = (uint32_t)nst * WB;
+        const uint32_t S_st = splits(c_in, pre < st_len ? pre : st_len);
+        for (uint32_t j = (uint32_t)lane; j < S_st; j += kWave) {
+            const uint64_t gi = h_in + j;
+            if (gi > 0) {
+                counts[gi - 1] = 255;
+                values[gi - 1] = (uint8_t)v0;
+            }
+        }
+        const uint64_t g0 = h_in + S_st;  // global index of the first natural head
+        if (Kst) {
+            if (lane == 0 && g0 > 0) {
+                const uint32_t c = add_c(c_in, first);
+                counts[g0 - 1] = (uint8_t)(c == 0 ? 255u : c);
+                values[g0 - 1] = stv[0];
+            }
+            for (uint32_t j = 1 + (uint32_t)lane; j < Kst; j += kWave) {
+                counts[g0 + j - 1] = stc[j];
+                values[g0 + j - 1] = stv[j];
+            }
+        }
+    }
+    if (nst < ns) {
+        // sub-chunks [nst, ns): re-read and emit with the true states
+        uint32_t rel = rel_st;
+        uint64_t hb = h_in + splits(c_in, pre < (uint32_t)nst * WB ? pre : (uint32_t)nst * WB) + Kst;
+        const uint64_t re_off = chunk_off + (uint64_t)nst * WB;
+        uint32_t pb = re_off > 0 ? (uint32_t)in[re_off - 1] : 0u;
+        load_sub(nst, pf);
+        for (int s = nst; s < ns; ++s) {
+            // the staged copy-out above and the previous sub-chunk's reads of the
+            // staging and the image are this wave's own LDS ops: in order
+            Sub L;
+            pb = scan_sub(s, L, pf, pb, s + 1 < ns);
+            const uint32_t c_lane = pm_apply(pm_compose(rel, L.lrel), c_in);
+            uint64_t hm0, hm1;
+            head_masks(L, c_lane, true, hm0, hm1);
+            const uint32_t hl = (uint32_t)(__popcll(hm0) + __popcll(hm1));
+            const uint32_t hincl = wave_incl_scan_u32(hl);
+            const uint32_t hs = (uint32_t)__builtin_amdgcn_readlane((int)hincl, kWave - 1);
+            const uint64_t g = hb + (hincl - hl);
+            if (hs <= (uint32_t)SW) {
+                // sparse: stage at (g - hb), store contiguously
+                lane_runs(L, hm0, hm1, c_lane, stc, stv, (uint32_t)(g - hb));
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                for (uint32_t j = lane; j < hs; j += kWave) {
+                    const uint64_t gi = hb + j;
+                    if (gi > 0) {
+                        counts[gi - 1] = stc[j];
+                        values[gi - 1] = stv[j];
+                    }
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            } else {
+                // dense: ONE lane row at a time, lane t taking byte positions t
+                // and 64 + t of the row (ranks by popcount): contiguous stores
+                const uint64_t below = ((uint64_t)1 << lane) - 1;
+#pragma unroll 1
+                for (int r = 0; r < kWave; ++r) {
+                    const uint64_t h0 = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(hm0 >> 32), r) << 32) |
+                                        (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)hm0, r);
+                    const uint64_t h1 = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(hm1 >> 32), r) << 32) |
+                                        (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)hm1, r);
+                    const uint64_t g_row = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(g >> 32), r) << 32) |
+                                           (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)g, r);
+                    const uint32_t c_row = (uint32_t)__builtin_amdgcn_readlane((int)c_lane, r);
+                    const uint32_t p_row = (uint32_t)__builtin_amdgcn_readlane((int)L.p0, r);
+                    const uint32_t rr = (uint32_t)r;
+                    const uint8_t *rowp = img + rr * LB;
+#pragma unroll
+                    for (int half = 0; half < 2; ++half) {
+                        const uint64_t hm = half ? h1 : h0;
+                        if ((hm >> lane) & 1u) {
+                            const uint64_t bl = hm & below;
+                            const uint32_t pos = (uint32_t)(half * 64 + lane);
+                            const uint32_t rank = (half ? (uint32_t)__popcll(h0) : 0u) + (uint32_t)__popcll(bl);
+                            int prev;
+                            if (bl)
+                                prev = half * 64 + 63 - __builtin_clzll(bl);
+                            else
+                                prev = (half && h0) ? 63 - __builtin_clzll(h0) : -1;
+                            uint32_t cnt = prev < 0 ? add_c(c_row, pos) : pos - (uint32_t)prev;
+                            cnt = cnt == 0 ? 255u : cnt;
+                            const uint32_t q = pos - 1;
+                            const uint32_t val = pos == 0 ? p_row : rowp[(((q >> 4) ^ (rr & 7u)) * 16) + (q & 15u)];
+                            const uint64_t gi = g_row + rank;
+                            if (gi > 0) {
+                                counts[gi - 1] = (uint8_t)cnt;
+                                values[gi - 1] = (uint8_t)val;
+                            }
+                        }
+                    }
+                }
+            }
+            hb += hs;
+            rel = pm_compose(rel, L.smap);
+        }
+    }
+
+    // ---- the final run (ends at byte n-1): the wave whose chunk holds it ----
+    if (chunk_off + chunk_len == n && lane == 0) {
+        const uint64_t R = h_in + splits(c_in, pre) + K;
+        const uint32_t c_end = pm_apply(rel_in, c_in);
+        counts[R - 1] = (uint8_t)(c_end == 0 ? 255u : c_end);
+        values[R - 1] = in[n - 1];
+        *runs_out = R;
+    }
+}
+
 // ---- decode pre-pass: output offsets of each decode tile ------------------
 // `iters` rounds of kRoRuns counts per workgroup; offsets are written
 // workgroup-relative, then the workgroup's base (block_prefix_all) is added.
@@ -1148,9 +1514,20 @@ extern "C" int flrl_rl_encode_device(const uint8_t *d_in, size_t n, uint8_t *d_c
         return set_error(FLRL_E_ARG, "flrl_rl_encode_device: input too large");
     Ctrl *ctrl = static_cast<Ctrl *>(d_scratch);
     uint64_t *status = reinterpret_cast<uint64_t *>(ctrl + 1);
+#ifdef FLRL_RL_ENCODE_V1  // A/B builds only (scripts/ab_libs.py)
+    constexpr bool v1 = true;
+#else
+    constexpr bool v1 = false;
+#endif
     kernel_timing_begin(s);
-    hipLaunchKernelGGL((rl_encode_kernel<kRlThreads, kRlLaneBytes, kRlSub>), dim3((uint32_t)L.tiles), dim3(kRlThreads),
-                       FLRL_RL_DYN_LDS, s, d_in, (uint64_t)n, (uint32_t)L.tiles, d_counts, d_values, d_runs, ctrl, status);
+    if (v1)
+        hipLaunchKernelGGL((rl_encode_kernel<kRlThreads, kRlLaneBytes, kRlSub>), dim3((uint32_t)L.tiles),
+                           dim3(kRlThreads), FLRL_RL_DYN_LDS, s, d_in, (uint64_t)n, (uint32_t)L.tiles, d_counts,
+                           d_values, d_runs, ctrl, status);
+    else
+        hipLaunchKernelGGL((rl_encode_wave_kernel<kRlThreads, kRlLaneBytes, kRlSub>), dim3((uint32_t)L.tiles),
+                           dim3(kRlThreads), 0, s, d_in, (uint64_t)n, (uint32_t)L.tiles, d_counts, d_values,
+                           d_runs, ctrl, status);
     kernel_timing_end(s);
     FLRL_HIP(hipGetLastError());
     return FLRL_OK;
