@@ -73,6 +73,17 @@ hipError_t zero_async(void *p, size_t bytes, hipStream_t s)
     return hipGetLastError();
 }
 
+static thread_local int g_skip_resets = 0;
+
+hipError_t scratch_reset(void *p, size_t bytes, hipStream_t s)
+{
+    if (g_skip_resets > 0) {
+        --g_skip_resets;
+        return hipSuccess;
+    }
+    return zero_async(p, bytes, s);
+}
+
 // splitmix64 draw number w+1 from `seed` (counter form of SURVEY.md §8(d)).
 __device__ __forceinline__ uint64_t splitmix_at(uint64_t seed, uint64_t w)
 {
@@ -111,6 +122,14 @@ extern "C" int flrl_time_next_kernel(void *start_event, void *stop_event)
         return set_error(FLRL_E_ARG, "flrl_time_next_kernel: pass both events or neither");
     g_ev_start = static_cast<hipEvent_t>(start_event);
     g_ev_stop = static_cast<hipEvent_t>(stop_event);
+    return FLRL_OK;
+}
+
+extern "C" int flrl_debug_skip_scratch_resets(int calls)
+{
+    if (calls < 0)
+        return set_error(FLRL_E_ARG, "flrl_debug_skip_scratch_resets: negative count");
+    g_skip_resets = calls;
     return FLRL_OK;
 }
 

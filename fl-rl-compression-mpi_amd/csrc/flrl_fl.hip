@@ -180,10 +180,16 @@ __global__ __launch_bounds__(T + kWave, 1) void fl_encode_kernel(
         s_next[0] = atomicAdd(&ctrl->ticket, 1u);
     __syncthreads();
     uint32_t tile = s_next[0];
-    // not an error: a workgroup dispatched late (the GPU shared with other
-    // work) can find every tile taken by the others
-    if (tile >= ntiles)
+    // a launch hands out exactly ntiles + gridDim.x tickets (each workgroup
+    // stops at its first ticket >= ntiles), so a first ticket past that means
+    // the scratch's ticket was not reset for this launch
+    if (tile >= ntiles) {
+        if ((uint64_t)tile >= (uint64_t)ntiles + gridDim.x && tid == 0)
+            raise_error(ctrl, FLRL_E_ARG);
+        // otherwise not an error: a workgroup dispatched late (the GPU shared
+        // with other work) can find every tile taken by the others
         return;
+    }
     uint32_t slot = 1;
     u32x4 a[ITEMS];
     if (!lw)
@@ -654,7 +660,7 @@ extern "C" int flrl_fl_encode_device(const uint8_t *d_in, size_t n, uint8_t *d_b
         return set_error(FLRL_E_ARG, "flrl_fl_encode_device: buffers must be 16-byte aligned");
     if (L.enc_tiles > 0xFFFFFFFFull)
         return set_error(FLRL_E_ARG, "flrl_fl_encode_device: input too large");
-    FLRL_HIP(zero_async(d_scratch, L.enc_zero, s));
+    FLRL_HIP(scratch_reset(d_scratch, L.enc_zero, s));
     Ctrl *ctrl = static_cast<Ctrl *>(d_scratch);
     uint64_t *status = reinterpret_cast<uint64_t *>(ctrl + 1);
     const size_t resident = (size_t)cu_count();
@@ -693,7 +699,7 @@ extern "C" int flrl_fl_decode_device(const uint8_t *d_bits, size_t bits_size,
         return set_error(FLRL_E_ARG, "flrl_fl_decode_device: buffers must be 16-byte aligned");
     if (L.dec_tiles > 0x7FFFFFFFull)
         return set_error(FLRL_E_ARG, "flrl_fl_decode_device: output too large");
-    FLRL_HIP(zero_async(d_scratch, L.dec_zero, s));
+    FLRL_HIP(scratch_reset(d_scratch, L.dec_zero, s));
     Ctrl *ctrl = static_cast<Ctrl *>(d_scratch);
     uint64_t *status = reinterpret_cast<uint64_t *>(ctrl + 1);
     uint64_t *tile_base =

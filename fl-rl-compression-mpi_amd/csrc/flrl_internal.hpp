@@ -21,6 +21,10 @@ void clear_error();
 // tightly around a device call's main kernel (no-ops when none are pending).
 // Zero `bytes` at device pointer p on stream s (a kernel, also inside graphs).
 hipError_t zero_async(void *p, size_t bytes, hipStream_t s);
+// The per-call scratch reset (ticket, error word, status granules) of a device
+// call: zero_async unless flrl_debug_skip_scratch_resets asked this thread to
+// skip it (tests of the kernels' stale-ticket checks).
+hipError_t scratch_reset(void *p, size_t bytes, hipStream_t s);
 
 void kernel_timing_begin(hipStream_t s);
 void kernel_timing_end(hipStream_t s);

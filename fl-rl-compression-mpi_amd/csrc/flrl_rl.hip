@@ -1501,7 +1501,7 @@ extern "C" int flrl_rl_encode_device(const uint8_t *d_in, size_t n, uint8_t *d_c
                          scratch_bytes, L.bytes);
     if (!aligned16(d_scratch))
         return set_error(FLRL_E_ARG, "flrl_rl_encode_device: scratch not 16-byte aligned");
-    FLRL_HIP(zero_async(d_scratch, L.bytes, s));
+    FLRL_HIP(scratch_reset(d_scratch, L.bytes, s));
     if (n == 0) {
         FLRL_HIP(zero_async(d_runs, sizeof(uint64_t), s));
         return FLRL_OK;
@@ -1546,7 +1546,7 @@ extern "C" int flrl_rl_decode_device(const uint8_t *d_counts, const uint8_t *d_v
                          scratch_bytes, L.bytes);
     if (!aligned16(d_scratch))
         return set_error(FLRL_E_ARG, "flrl_rl_decode_device: scratch not 16-byte aligned");
-    FLRL_HIP(zero_async(d_scratch, L.zero, s));
+    FLRL_HIP(scratch_reset(d_scratch, L.zero, s));
     if (runs == 0) {
         if (n != 0) {
             const uint32_t e = FLRL_E_FORMAT;

@@ -133,7 +133,10 @@ int dev_setup(Dev &d, size_t gather_entries)
         if (hipMalloc(&d.gather, gather_entries * sizeof(uint64_t)) != hipSuccess)
             return set_error(FLRL_E_NOMEM, "Cannot allocate memory (device %d)", d.id);
         d.gather_cap = gather_entries;
-        if (hipMemset(d.gather, 0, gather_entries * sizeof(uint64_t)) != hipSuccess)
+        // complete before returning: the shards' streams are non-blocking, so a
+        // null-stream hipMemset could land after their first size writes
+        if (hipMemsetAsync(d.gather, 0, gather_entries * sizeof(uint64_t), d.cstream) != hipSuccess ||
+            hipStreamSynchronize(d.cstream) != hipSuccess)
             return set_error(FLRL_E_HIP, "hipMemset failed on device %d", d.id);
     }
     return FLRL_OK;

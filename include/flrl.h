@@ -214,6 +214,13 @@ int flrl_scratch_error(const void *d_scratch, void *stream);
  * NULL cancels a pending pair. */
 int flrl_time_next_kernel(void *start_event, void *stop_event);
 
+/* Test hook (no reference counterpart): the next `calls` device calls of this
+ * thread skip their per-call scratch reset, so their kernels see the previous
+ * launch's ticket. Every ticketed kernel then raises FLRL_E_ARG in the scratch
+ * error word instead of running (or silently doing nothing) on stale state.
+ * 0 cancels. Never needed by callers. */
+int flrl_debug_skip_scratch_resets(int calls);
+
 /* ---- RL, host buffers (synchronous) --------------------------------------- */
 int flrl_rl_compress(const uint8_t *data, size_t size, flrl_rl_buf *out);
 int flrl_rl_decompress(size_t output_size, const uint8_t *counts, const uint8_t *values,

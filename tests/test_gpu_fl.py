@@ -177,6 +177,49 @@ def test_device_bad_width_flag():
     assert d.error() == flrl.E_FORMAT
 
 
+@pytest.mark.parametrize("n", [5000, (8 << 20) + 5])
+def test_stale_scratch_raises(n):
+    """A launch on scratch whose ticket was not reset (flrl_debug_skip_scratch_resets)
+    flags FLRL_E_ARG in every ticketed kernel (FL encode included: it used to
+    return silently when every first ticket was past the grid); the next
+    normal call resets the scratch and runs bit-exact again."""
+    from flrl.device import FLDevice, RLDevice
+    a = oracle.gen("lo4", n, 9)
+    x = torch.from_numpy(a).cuda()
+    d = FLDevice(n)
+    d.encode(x)
+    v = d.values_size()
+    assert d.error() == 0
+    bits0, vals0 = d.bits[:d.frames].clone(), d.values[:v].clone()
+    flrl.debug_skip_scratch_resets(1)
+    d.encode(x)
+    assert d.error() == flrl.E_ARG
+    d.encode(x)
+    assert d.error() == 0 and d.values_size() == v
+    assert torch.equal(d.bits[:d.frames], bits0) and torch.equal(d.values[:v], vals0)
+    assert torch.equal(d.decode(v), x) and d.error() == 0
+    flrl.debug_skip_scratch_resets(1)
+    d.decode(v)
+    assert d.error() == flrl.E_ARG
+    assert torch.equal(d.decode(v), x) and d.error() == 0
+
+    r = RLDevice(n)
+    r.encode(x)
+    R = r.runs()
+    assert r.error() == 0
+    flrl.debug_skip_scratch_resets(1)
+    r.encode(x)
+    assert r.error() == flrl.E_ARG
+    r.encode(x)
+    assert r.error() == 0 and r.runs() == R
+    assert torch.equal(r.decode(R), x) and r.error() == 0
+    flrl.debug_skip_scratch_resets(1)
+    r.decode(R)
+    assert r.error() == flrl.E_ARG
+    assert torch.equal(r.decode(R), x) and r.error() == 0
+    flrl.debug_skip_scratch_resets(0)
+
+
 @pytest.mark.parametrize("idx", [0, 1])
 def test_device_1gib_golden(golden, idx):
     """Config #2 (u8) and the lo4 twin at 1 GiB: file sha256 == reference fl-cpu."""
