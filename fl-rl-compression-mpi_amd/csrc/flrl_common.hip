@@ -125,6 +125,16 @@ extern "C" int flrl_time_next_kernel(void *start_event, void *stop_event)
     return FLRL_OK;
 }
 
+static std::atomic<long long> g_fail_chunk{-1};
+
+bool flrl::debug_fail_chunk(size_t c) { return (long long)c == g_fail_chunk.load(std::memory_order_relaxed); }
+
+extern "C" int flrl_debug_fail_chunk(long long chunk)
+{
+    g_fail_chunk.store(chunk < 0 ? -1 : chunk);
+    return FLRL_OK;
+}
+
 extern "C" int flrl_debug_skip_scratch_resets(int calls)
 {
     if (calls < 0)

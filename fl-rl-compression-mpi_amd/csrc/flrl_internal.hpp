@@ -25,6 +25,8 @@ hipError_t zero_async(void *p, size_t bytes, hipStream_t s);
 // call: zero_async unless flrl_debug_skip_scratch_resets asked this thread to
 // skip it (tests of the kernels' stale-ticket checks).
 hipError_t scratch_reset(void *p, size_t bytes, hipStream_t s);
+// flrl_debug_fail_chunk: true when the streamed file paths should fail chunk c.
+bool debug_fail_chunk(size_t c);
 
 void kernel_timing_begin(hipStream_t s);
 void kernel_timing_end(hipStream_t s);

@@ -1,0 +1,128 @@
+// flrl_outfile.hpp — output files that appear whole or not at all.
+//
+// The reference loads the whole input before it opens the output
+// (src/main.cu:72-129, src/file_io.cu:194-280), so `compress c fl f f` works
+// there and a failed run leaves an existing output alone. The streamed file
+// paths here read the input while writing, so they write to a temporary file
+// next to the output (same directory, so rename() is atomic on one file
+// system) and rename it into place only on success; on failure the temporary
+// is unlinked and a pre-existing output is untouched. An existing output that
+// is not a regular file (/dev/null, a FIFO) is written directly.
+// Header-only (POSIX), shared by libflrl.so and the CLI.
+#pragma once
+
+#include <fcntl.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <string>
+#include <vector>
+
+namespace flrl {
+
+// Creation mode of a new output: 0666 & ~umask, as fopen(path, "wb") would
+// give (read from /proc/self/status rather than set-and-restore umask, which
+// would race other threads creating files).
+inline mode_t new_file_mode()
+{
+    mode_t mask = 022;
+    if (FILE *f = fopen("/proc/self/status", "r")) {
+        char line[128];
+        while (fgets(line, sizeof(line), f))
+            if (strncmp(line, "Umask:", 6) == 0) {
+                mask = (mode_t)strtoul(line + 6, nullptr, 8);
+                break;
+            }
+        fclose(f);
+    }
+    return 0666 & ~mask;
+}
+
+class OutFile {
+public:
+    int fd = -1;
+
+    OutFile() = default;
+    OutFile(const OutFile &) = delete;
+    OutFile &operator=(const OutFile &) = delete;
+    ~OutFile()
+    {
+        if (fd >= 0)
+            ::close(fd);
+        if (!done_ && !tmp_.empty())
+            ::unlink(tmp_.c_str());
+    }
+
+    // false (errno set) when the output cannot be created
+    bool open(const char *path, bool read_write = false)
+    {
+        path_ = path;
+        struct stat st;
+        if (::stat(path, &st) == 0 && !S_ISREG(st.st_mode)) {
+            direct_ = true;
+            fd = ::open(path, read_write ? O_RDWR : O_WRONLY);
+            return fd >= 0;
+        }
+        const size_t slash = path_.rfind('/');
+        const std::string dir = slash == std::string::npos ? "." : (slash == 0 ? "/" : path_.substr(0, slash));
+        const std::string base = slash == std::string::npos ? path_ : path_.substr(slash + 1);
+        std::string t = dir + "/." + base + ".flrl-XXXXXX";
+        std::vector<char> buf(t.begin(), t.end());
+        buf.push_back('\0');
+        fd = ::mkstemp(buf.data());
+        if (fd < 0)
+            return false;
+        tmp_ = buf.data();
+        (void)::fchmod(fd, new_file_mode());
+        return true;
+    }
+
+    // set the file length (no-op for a non-regular output)
+    bool truncate(uint64_t len) { return direct_ || ::ftruncate(fd, (off_t)len) == 0; }
+
+    // close (unless the caller already did, fd = -1) and move into place;
+    // false (nothing replaced) on failure
+    bool commit()
+    {
+        if (fd >= 0) {
+            const int f = fd;
+            fd = -1;
+            if (::close(f) != 0)
+                return false;
+        }
+        if (!direct_ && ::rename(tmp_.c_str(), path_.c_str()) != 0)
+            return false;
+        done_ = true;
+        return true;
+    }
+
+private:
+    std::string path_, tmp_;
+    bool direct_ = false, done_ = false;
+};
+
+// An anonymous scratch file in the directory of `near_path` (unlinked at once,
+// so it never collides with or clobbers a user file). -1 on failure.
+inline int anon_file_near(const char *near_path)
+{
+    std::string p(near_path);
+    const size_t slash = p.rfind('/');
+    const std::string dir = slash == std::string::npos ? "." : (slash == 0 ? "/" : p.substr(0, slash));
+#ifdef O_TMPFILE
+    const int t = ::open(dir.c_str(), O_TMPFILE | O_RDWR, 0600);
+    if (t >= 0)
+        return t;
+#endif
+    std::string s = dir + "/.flrl-side-XXXXXX";
+    std::vector<char> buf(s.begin(), s.end());
+    buf.push_back('\0');
+    const int fd = ::mkstemp(buf.data());
+    if (fd >= 0)
+        ::unlink(buf.data());
+    return fd;
+}
+
+}  // namespace flrl

@@ -11,14 +11,17 @@
 //              overlaps the next chunk's read and H2D); a writer places bits at
 //              24 + chunk_start/128 and values at 24 + F + (values of earlier
 //              chunks) with pwrite, in chunk order, and writes the header last.
-//   decompress header + bits are read once; value offsets of every chunk come
-//              from a host prefix over the widths (16 bytes per full frame);
-//              each chunk is then decoded independently and pwritten at its
-//              input offset.
+//   decompress the header, then one streamed pass over the widths gives every
+//              chunk's value offset (a host prefix, 16 bytes per width unit);
+//              each chunk (its widths and values read by its worker) is then
+//              decoded independently and pwritten at its input offset.
 // Chunks are frame-aligned, so the file is byte-identical to a whole-input
 // encode (the concatenation identity). Memory is bounded
 // by the chunk size (per worker: 2 x (2 chunks + chunk/128) pinned host bytes
 // and as much device memory), so files larger than host RAM or HBM stream.
+// Outputs are written to a temporary file next to the output and renamed into
+// place on success (flrl_outfile.hpp): a failed call leaves an existing output
+// untouched, and the input may be the output.
 #include <fcntl.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -36,6 +39,7 @@
 
 #include "flrl.h"
 #include "flrl_internal.hpp"
+#include "flrl_outfile.hpp"
 
 namespace flrl {
 namespace {
@@ -127,6 +131,14 @@ int worker_count(int workers, int *ndev)
     return workers > 0 ? workers : *ndev;
 }
 
+// Pipelines actually started: min(W, units), at least 1 (size_t: the unit
+// count of a huge file with a small chunk can exceed INT_MAX).
+int pipelines(int W, size_t units)
+{
+    const size_t u = units ? units : 1;
+    return (size_t)W < u ? W : (int)u;
+}
+
 // Per-worker buffers: two slots, each with its stream, pinned host staging and
 // device buffers.
 struct Slot {
@@ -188,6 +200,22 @@ struct Ready {
     std::atomic<bool> *released = nullptr;  // set by the writer once written
 };
 
+// The in-order writer has stopped (done, or after a failure): every chunk
+// handed over but not written is released, and chunks finished later are not
+// handed over, so no worker waits for a writer that is gone.
+void release_unwritten(std::mutex &m, std::condition_variable &cv, std::vector<Ready> &ready,
+                       bool &writer_stopped)
+{
+    {
+        std::lock_guard<std::mutex> g(m);
+        writer_stopped = true;
+        for (Ready &r : ready)
+            if (r.done && r.released)
+                r.released->store(true);
+    }
+    cv.notify_all();
+}
+
 }  // namespace
 }  // namespace flrl
 
@@ -203,14 +231,15 @@ extern "C" int flrl_fl_compress_file(const char *in_path, const char *out_path, 
     const int W = worker_count(workers, &ndev);
     if (W <= 0)
         return set_error(FLRL_E_NODEV, "flrl_fl_compress_file: no HIP device");
-    Fd in, out;
+    Fd in;
+    OutFile out;
     if ((in.fd = ::open(in_path, O_RDONLY)) < 0)
         return set_error(FLRL_E_ARG, "[FileIO] Cannot open file: %s", in_path);
     struct stat st;
     if (::fstat(in.fd, &st) != 0)
         return set_error(FLRL_E_ARG, "[FileIO] Cannot stat file: %s", in_path);
     const uint64_t n = (uint64_t)st.st_size;
-    if ((out.fd = ::open(out_path, O_WRONLY | O_CREAT | O_TRUNC, 0644)) < 0)
+    if (!out.open(out_path))
         return set_error(FLRL_E_ARG, "[FileIO] Cannot open file: %s", out_path);
     const uint64_t F = (n + kFrame - 1) / kFrame;
     const size_t chunk = chunk_size(chunk_bytes);
@@ -222,10 +251,11 @@ extern "C" int flrl_fl_compress_file(const char *in_path, const char *out_path, 
     fail.wait_m = &m;
     fail.wait_cv = &cv;
     std::vector<Ready> ready(nchunks);
-    const int nw = (int)(W < (int)(nchunks ? nchunks : 1) ? W : (nchunks ? nchunks : 1));
+    const int nw = pipelines(W, nchunks);
     std::vector<std::atomic<bool>> slot_free((size_t)nw * 2);
     for (auto &f : slot_free)
         f.store(true);
+    bool writer_stopped = false;  // under m: chunks handed over later are never read
 
     auto worker = [&](int w) {
         if (hipSetDevice(w % ndev) != hipSuccess) {
@@ -257,9 +287,10 @@ extern "C" int flrl_fl_compress_file(const char *in_path, const char *out_path, 
                 hipStreamSynchronize(x.s) != hipSuccess)
                 return false;
             std::atomic<bool> *rel = &slot_free[(size_t)w * 2 + k];
-            rel->store(false);
             {
                 std::lock_guard<std::mutex> g(m);
+                if (!writer_stopped)
+                    rel->store(false);
                 Ready &r = ready[c];
                 r.bits = x.h_b;
                 r.nbits = fb;
@@ -285,6 +316,10 @@ extern "C" int flrl_fl_compress_file(const char *in_path, const char *out_path, 
                 break;
             const uint64_t off = (uint64_t)c * chunk;
             const size_t len = (size_t)((c + 1 == nchunks) ? n - off : chunk);
+            if (debug_fail_chunk(c)) {
+                fail.set(FLRL_E_HIP, "injected failure (flrl_debug_fail_chunk)");
+                break;
+            }
             if (!pread_all(in.fd, x.h_a, len, off)) {
                 fail.set(FLRL_E_ARG, "[FileIO] Cannot read file content");
                 break;
@@ -305,12 +340,10 @@ extern "C" int flrl_fl_compress_file(const char *in_path, const char *out_path, 
         }
         if (!fail.failed.load() && pend != SIZE_MAX && !finish(pend, pend_k))
             fail.set(FLRL_E_HIP, "fl encode: stream failed");
-        // keep the buffers alive until the writer has written them
+        // keep the pinned buffers alive until the writer has released them
+        // (also after a failure: the writer may still be reading one of them)
         std::unique_lock<std::mutex> g(m);
-        cv.wait(g, [&] {
-            return fail.failed.load() ||
-                   (slot_free[(size_t)w * 2].load() && slot_free[(size_t)w * 2 + 1].load());
-        });
+        cv.wait(g, [&] { return slot_free[(size_t)w * 2].load() && slot_free[(size_t)w * 2 + 1].load(); });
     };
 
     std::vector<std::thread> threads;
@@ -346,18 +379,14 @@ extern "C" int flrl_fl_compress_file(const char *in_path, const char *out_path, 
         }
         cv.notify_all();
     }
+    release_unwritten(m, cv, ready, writer_stopped);
     for (auto &t : threads)
         t.join();
     if (fail.failed.load())
         return set_error(fail.code ? fail.code : FLRL_E_HIP, "%s", fail.msg.c_str());
     const uint64_t hdr[3] = {n, F, voff};
-    if (!pwrite_all(out.fd, hdr, sizeof(hdr), 0) || ::ftruncate(out.fd, (off_t)(kHeader + F + voff)) != 0)
+    if (!pwrite_all(out.fd, hdr, sizeof(hdr), 0) || !out.truncate(kHeader + F + voff) || !out.commit())
         return set_error(FLRL_E_ARG, "[FileIO] Cannot write to file");
-    if (::close(out.fd) != 0) {
-        out.fd = -1;
-        return set_error(FLRL_E_ARG, "[FileIO] Cannot write to file");
-    }
-    out.fd = -1;
     return FLRL_OK;
 }
 
@@ -371,7 +400,8 @@ extern "C" int flrl_fl_decompress_file(const char *in_path, const char *out_path
     const int W = worker_count(workers, &ndev);
     if (W <= 0)
         return set_error(FLRL_E_NODEV, "flrl_fl_decompress_file: no HIP device");
-    Fd in, out;
+    Fd in;
+    OutFile out;
     if ((in.fd = ::open(in_path, O_RDONLY)) < 0)
         return set_error(FLRL_E_ARG, "[FileIO] Cannot open file: %s", in_path);
     struct stat st;
@@ -389,48 +419,52 @@ extern "C" int flrl_fl_decompress_file(const char *in_path, const char *out_path
                          "file %llu bytes)",
                          (unsigned long long)n, (unsigned long long)F, (unsigned long long)V,
                          (unsigned long long)fsize);
-    if ((out.fd = ::open(out_path, O_WRONLY | O_CREAT | O_TRUNC, 0644)) < 0)
+    if (!out.open(out_path))
         return set_error(FLRL_E_ARG, "[FileIO] Cannot open file: %s", out_path);
     if (n == 0 || V == 0) {  // the reference's early-out: empty result (fl_cpu.cu:94-97)
-        if (::close(out.fd) != 0) {
-            out.fd = -1;
+        if (!out.commit())
             return set_error(FLRL_E_ARG, "[FileIO] Cannot write to file");
-        }
-        out.fd = -1;
         return FLRL_OK;
     }
     const size_t chunk = chunk_size(chunk_bytes);
     const size_t cf = chunk / kFrame;  // frames per chunk
     const size_t nchunks = (size_t)((n + chunk - 1) / chunk);
-    // widths once; value offset of every chunk = 16 x (widths of all earlier frames)
-    std::vector<uint8_t> bits((size_t)F);
-    if (!pread_all(in.fd, bits.data(), (size_t)F, kHeader))
-        return set_error(FLRL_E_ARG, "[FileIO] Cannot read file content");
+    // value offset of every chunk = 16 x (widths of all earlier frames): one
+    // streamed pass over the widths (host memory bounded by a 4 MiB window, not
+    // F = n/128 bytes); the workers then read each chunk's widths themselves
     std::vector<uint64_t> voff(nchunks + 1);
     {
-        uint64_t acc = 0;
-        for (size_t c = 0; c < nchunks; ++c) {
-            voff[c] = acc;
-            const size_t f1 = (c + 1) * cf < F ? (c + 1) * cf : (size_t)F;
-            uint64_t s = 0;
-            for (size_t f = c * cf; f < f1; ++f) {
-                const uint8_t b = bits[f];
+        std::vector<uint8_t> win(4u << 20);
+        uint64_t acc = 0, cur = 0;  // cur: width sum of the current chunk so far
+        for (uint64_t f0 = 0; f0 < F;) {
+            const size_t k = (size_t)(F - f0 < win.size() ? F - f0 : win.size());
+            if (!pread_all(in.fd, win.data(), k, kHeader + f0))
+                return set_error(FLRL_E_ARG, "[FileIO] Cannot read file content");
+            for (size_t i = 0; i < k; ++i) {
+                const uint64_t f = f0 + i;
+                if (f % cf == 0) {
+                    acc += 16 * cur;
+                    voff[(size_t)(f / cf)] = acc;
+                    cur = 0;
+                }
+                const uint8_t b = win[i];
                 if (b < 1 || b > 8)
-                    return set_error(FLRL_E_FORMAT, "invalid frame width %u at frame %zu", b, f);
-                s += b;
+                    return set_error(FLRL_E_FORMAT, "invalid frame width %u at frame %llu", b,
+                                     (unsigned long long)f);
+                cur += b;
             }
-            acc += 16 * s;
+            f0 += k;
         }
         voff[nchunks] = V;
         if (voff[nchunks - 1] > V)
             return set_error(FLRL_E_FORMAT, "valuesSize %llu smaller than the widths imply",
                              (unsigned long long)V);
     }
-    if (::ftruncate(out.fd, (off_t)n) != 0)
+    if (!out.truncate(n))
         return set_error(FLRL_E_ARG, "[FileIO] Cannot write to file");
 
     Failure fail;
-    const int nw = (int)(W < (int)nchunks ? W : (int)nchunks);
+    const int nw = pipelines(W, nchunks);
     auto worker = [&](int w) {
         if (hipSetDevice(w % ndev) != hipSuccess) {
             fail.set(FLRL_E_HIP, "hipSetDevice failed");
@@ -476,8 +510,12 @@ extern "C" int flrl_fl_decompress_file(const char *in_path, const char *out_path
                 fail.set(FLRL_E_FORMAT, "valuesSize larger than the widths imply");
                 break;
             }
-            memcpy(x.h_a, bits.data() + c * cf, fb);
-            if (!pread_all(in.fd, x.h_b, (size_t)vb, kHeader + F + vo)) {
+            if (debug_fail_chunk(c)) {
+                fail.set(FLRL_E_HIP, "injected failure (flrl_debug_fail_chunk)");
+                break;
+            }
+            if (!pread_all(in.fd, x.h_a, fb, kHeader + (uint64_t)c * cf) ||
+                !pread_all(in.fd, x.h_b, (size_t)vb, kHeader + F + vo)) {
                 fail.set(FLRL_E_ARG, "[FileIO] Cannot read file content");
                 break;
             }
@@ -504,11 +542,8 @@ extern "C" int flrl_fl_decompress_file(const char *in_path, const char *out_path
         t.join();
     if (fail.failed.load())
         return set_error(fail.code ? fail.code : FLRL_E_HIP, "%s", fail.msg.c_str());
-    if (::close(out.fd) != 0) {
-        out.fd = -1;
+    if (!out.commit())
         return set_error(FLRL_E_ARG, "[FileIO] Cannot write to file");
-    }
-    out.fd = -1;
     return FLRL_OK;
 }
 
@@ -610,19 +645,19 @@ extern "C" int flrl_rl_compress_file(const char *in_path, const char *out_path, 
     const int W = worker_count(workers, &ndev);
     if (W <= 0)
         return set_error(FLRL_E_NODEV, "flrl_rl_compress_file: no HIP device");
-    Fd in, out, side;
+    Fd in, side;
+    OutFile out;
     if ((in.fd = ::open(in_path, O_RDONLY)) < 0)
         return set_error(FLRL_E_ARG, "[FileIO] Cannot open file: %s", in_path);
     struct stat st;
     if (::fstat(in.fd, &st) != 0)
         return set_error(FLRL_E_ARG, "[FileIO] Cannot stat file: %s", in_path);
     const uint64_t n = (uint64_t)st.st_size;
-    if ((out.fd = ::open(out_path, O_RDWR | O_CREAT | O_TRUNC, 0644)) < 0)
+    if (!out.open(out_path))
         return set_error(FLRL_E_ARG, "[FileIO] Cannot open file: %s", out_path);
-    const std::string side_path = std::string(out_path) + ".values.tmp";
-    if ((side.fd = ::open(side_path.c_str(), O_RDWR | O_CREAT | O_TRUNC, 0600)) < 0)
-        return set_error(FLRL_E_ARG, "[FileIO] Cannot open file: %s", side_path.c_str());
-    ::unlink(side_path.c_str());  // anonymous from here on
+    // values[] until R is known: an anonymous file next to the output
+    if ((side.fd = anon_file_near(out_path)) < 0)
+        return set_error(FLRL_E_ARG, "[FileIO] Cannot create a temporary file next to %s", out_path);
     const size_t chunk = requested_or(chunk_bytes);
     const size_t nchunks = n ? (size_t)((n + chunk - 1) / chunk) : 0;
 
@@ -632,10 +667,11 @@ extern "C" int flrl_rl_compress_file(const char *in_path, const char *out_path, 
     fail.wait_m = &m;
     fail.wait_cv = &cv;
     std::vector<Ready> ready(nchunks);
-    const int nw = (int)(W < (int)(nchunks ? nchunks : 1) ? W : (nchunks ? nchunks : 1));
+    const int nw = pipelines(W, nchunks);
     std::vector<std::atomic<bool>> slot_free((size_t)nw * 2);
     for (auto &f : slot_free)
         f.store(true);
+    bool writer_stopped = false;  // under m: chunks handed over later are never read
 
     auto worker = [&](int w) {
         if (hipSetDevice(w % ndev) != hipSuccess) {
@@ -664,9 +700,10 @@ extern "C" int flrl_rl_compress_file(const char *in_path, const char *out_path, 
                 hipStreamSynchronize(x.s) != hipSuccess)
                 return false;
             std::atomic<bool> *rel = &slot_free[(size_t)w * 2 + k];
-            rel->store(false);
             {
                 std::lock_guard<std::mutex> g(m);
+                if (!writer_stopped)
+                    rel->store(false);
                 Ready &r = ready[c];
                 r.bits = x.h_b;  // counts
                 r.values = x.h_c;
@@ -691,6 +728,10 @@ extern "C" int flrl_rl_compress_file(const char *in_path, const char *out_path, 
                 break;
             const uint64_t off = (uint64_t)c * chunk;
             const size_t len = (size_t)((c + 1 == nchunks) ? n - off : chunk);
+            if (debug_fail_chunk(c)) {
+                fail.set(FLRL_E_HIP, "injected failure (flrl_debug_fail_chunk)");
+                break;
+            }
             if (!pread_all(in.fd, x.h_a, len, off)) {
                 fail.set(FLRL_E_ARG, "[FileIO] Cannot read file content");
                 break;
@@ -711,10 +752,7 @@ extern "C" int flrl_rl_compress_file(const char *in_path, const char *out_path, 
         if (!fail.failed.load() && pend != SIZE_MAX && !finish(pend, pend_k))
             fail.set(FLRL_E_HIP, "rl encode: stream failed");
         std::unique_lock<std::mutex> g(m);
-        cv.wait(g, [&] {
-            return fail.failed.load() ||
-                   (slot_free[(size_t)w * 2].load() && slot_free[(size_t)w * 2 + 1].load());
-        });
+        cv.wait(g, [&] { return slot_free[(size_t)w * 2].load() && slot_free[(size_t)w * 2 + 1].load(); });
     };
     std::vector<std::thread> threads;
     for (int w = 0; w < nw && nchunks; ++w)
@@ -747,6 +785,7 @@ extern "C" int flrl_rl_compress_file(const char *in_path, const char *out_path, 
             break;
         }
     }
+    release_unwritten(m, cv, ready, writer_stopped);
     for (auto &t : threads)
         t.join();
     if (fail.failed.load())
@@ -767,13 +806,8 @@ extern "C" int flrl_rl_compress_file(const char *in_path, const char *out_path, 
             o += k;
         }
     }
-    if (::ftruncate(out.fd, (off_t)(16 + 2 * R)) != 0)
+    if (!out.truncate(16 + 2 * R) || !out.commit())
         return set_error(FLRL_E_ARG, "[FileIO] Cannot write to file");
-    if (::close(out.fd) != 0) {
-        out.fd = -1;
-        return set_error(FLRL_E_ARG, "[FileIO] Cannot write to file");
-    }
-    out.fd = -1;
     return FLRL_OK;
 }
 
@@ -787,7 +821,8 @@ extern "C" int flrl_rl_decompress_file(const char *in_path, const char *out_path
     const int W = worker_count(workers, &ndev);
     if (W <= 0)
         return set_error(FLRL_E_NODEV, "flrl_rl_decompress_file: no HIP device");
-    Fd in, out;
+    Fd in;
+    OutFile out;
     if ((in.fd = ::open(in_path, O_RDONLY)) < 0)
         return set_error(FLRL_E_ARG, "[FileIO] Cannot open file: %s", in_path);
     struct stat st;
@@ -836,13 +871,13 @@ extern "C" int flrl_rl_decompress_file(const char *in_path, const char *out_path
             return set_error(FLRL_E_FORMAT, "RL counts sum to %llu, header says %llu",
                              (unsigned long long)out_pos, (unsigned long long)n);
     }
-    if ((out.fd = ::open(out_path, O_WRONLY | O_CREAT | O_TRUNC, 0644)) < 0)
+    if (!out.open(out_path))
         return set_error(FLRL_E_ARG, "[FileIO] Cannot open file: %s", out_path);
-    if (::ftruncate(out.fd, (off_t)n) != 0)
+    if (!out.truncate(n))
         return set_error(FLRL_E_ARG, "[FileIO] Cannot write to file");
     const size_t nb = blocks.size();
     Failure fail;
-    const int nw = nb ? (int)(W < (int)nb ? W : (int)nb) : 0;
+    const int nw = nb ? pipelines(W, nb) : 0;
     auto worker = [&](int w) {
         if (hipSetDevice(w % ndev) != hipSuccess) {
             fail.set(FLRL_E_HIP, "hipSetDevice failed");
@@ -881,6 +916,10 @@ extern "C" int flrl_rl_decompress_file(const char *in_path, const char *out_path
             Slot &x = S.slot[k];
             const size_t nr = (size_t)(blocks[b].r1 - blocks[b].r0);
             const size_t len = len_of(b);
+            if (debug_fail_chunk(b)) {
+                fail.set(FLRL_E_HIP, "injected failure (flrl_debug_fail_chunk)");
+                break;
+            }
             if (!pread_all(in.fd, x.h_a, nr, 16 + blocks[b].r0) ||
                 !pread_all(in.fd, x.h_b, nr, 16 + R + blocks[b].r0)) {
                 fail.set(FLRL_E_ARG, "[FileIO] Cannot read file content");
@@ -908,10 +947,7 @@ extern "C" int flrl_rl_decompress_file(const char *in_path, const char *out_path
         t.join();
     if (fail.failed.load())
         return set_error(fail.code ? fail.code : FLRL_E_HIP, "%s", fail.msg.c_str());
-    if (::close(out.fd) != 0) {
-        out.fd = -1;
+    if (!out.commit())
         return set_error(FLRL_E_ARG, "[FileIO] Cannot write to file");
-    }
-    out.fd = -1;
     return FLRL_OK;
 }

@@ -111,6 +111,7 @@ _sig("flrl_fl_decode_device", ctypes.c_int, _vp, _sz, _vp, _sz, _vp, _sz, _vp, _
 _sig("flrl_scratch_error", ctypes.c_int, _vp, _vp)
 _sig("flrl_time_next_kernel", ctypes.c_int, _vp, _vp)
 _sig("flrl_debug_skip_scratch_resets", ctypes.c_int, ctypes.c_int)
+_sig("flrl_debug_fail_chunk", ctypes.c_int, ctypes.c_longlong)
 _sig("flrl_rl_compress", ctypes.c_int, _vp, _sz, ctypes.POINTER(_RLBuf))
 _sig("flrl_rl_decompress", ctypes.c_int, _sz, _vp, _vp, _sz,
      ctypes.POINTER(_u8p), ctypes.POINTER(_sz))
@@ -422,6 +423,11 @@ def time_next_kernel(start=None, stop=None) -> None:
 def debug_skip_scratch_resets(calls: int) -> None:
     """Test hook: this thread's next `calls` device calls skip their scratch reset."""
     _check(_lib.flrl_debug_skip_scratch_resets(calls))
+
+
+def debug_fail_chunk(chunk: int) -> None:
+    """Test hook: the streamed file paths fail at `chunk` (negative: never)."""
+    _check(_lib.flrl_debug_fail_chunk(chunk))
 
 
 def scratch_error(d_scratch: int, stream: int = 0) -> int:

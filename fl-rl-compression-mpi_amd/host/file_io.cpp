@@ -4,7 +4,10 @@
 // writes inputSize, bitsSize, valuesSize as host-endian u64 and then the two
 // arrays; :117-192 reads them back). Loading additionally checks the declared
 // sizes against the file length before allocating, so a truncated or corrupt
-// header fails with a message instead of reading out of bounds.
+// header fails with a message instead of reading out of bounds. Saving writes a
+// temporary file next to the output and renames it into place when complete
+// (flrl_outfile.hpp), so a failed run never truncates or removes an existing
+// output.
 #include "file_io.hpp"
 
 #include <cstdio>
@@ -13,17 +16,20 @@
 #include <stdexcept>
 #include <string>
 
+#include "flrl_outfile.hpp"
+
 namespace flrl_cli {
 
 namespace {
 
 struct File {
-    FILE *f;
+    FILE *f = nullptr;
     explicit File(const char *path, const char *mode) : f(std::fopen(path, mode))
     {
         if (!f)
             throw std::runtime_error(std::string("[FileIO] Cannot open file: ") + path);
     }
+    File() = default;
     ~File()
     {
         if (f)
@@ -57,6 +63,29 @@ struct File {
     }
 };
 
+// An output file: buffered writes into a temporary next to `path`, moved into
+// place by close().
+struct OutputFile {
+    flrl::OutFile out;
+    File file;
+    explicit OutputFile(const char *path)
+    {
+        if (!out.open(path))
+            throw std::runtime_error(std::string("[FileIO] Cannot open file: ") + path);
+        file.f = fdopen(out.fd, "wb");
+        if (!file.f)
+            throw std::runtime_error(std::string("[FileIO] Cannot open file: ") + path);
+        out.fd = -1;  // owned by the FILE from here on
+    }
+    void write(const void *src, size_t bytes) { file.write(src, bytes); }
+    void close()
+    {
+        file.close();  // fclose: the descriptor is closed with the FILE
+        if (!out.commit())
+            throw std::runtime_error("[FileIO] Cannot write to file");
+    }
+};
+
 uint8_t *alloc_bytes(size_t n)
 {
     uint8_t *p = static_cast<uint8_t *>(std::malloc(n ? n : 1));
@@ -84,7 +113,7 @@ FileData loadFile(const char *path)
 
 void saveFile(const char *path, const FileData &fd)
 {
-    File f(path, "wb");
+    OutputFile f(path);
     f.write(fd.data, fd.size);
     f.close();
 }
@@ -122,7 +151,7 @@ flrl_fl_buf loadCompressedFL(const char *path)
 
 void saveCompressedFL(const char *path, const flrl_fl_buf &c)
 {
-    File f(path, "wb");
+    OutputFile f(path);
     const uint64_t hdr[3] = {c.input_size, c.bits_size, c.values_size};
     f.write(hdr, sizeof(hdr));
     f.write(c.bits, c.bits_size);
@@ -162,7 +191,7 @@ flrl_rl_buf loadCompressedRL(const char *path)
 
 void saveCompressedRL(const char *path, const flrl_rl_buf &c)
 {
-    File f(path, "wb");
+    OutputFile f(path);
     const uint64_t hdr[2] = {c.input_size, c.runs};
     f.write(hdr, sizeof(hdr));
     f.write(c.counts, c.runs);

@@ -10,8 +10,9 @@
 // neither the file nor its output is held in memory; FLRL_CHUNK_BYTES and FLRL_WORKERS override the chunk size (64 MiB)
 // and the pipeline count. Errors print
 // "[ERROR]: <message>" to stderr like the reference (main.cu:95-98), but the
-// process then exits with status 2 instead of 0, and no partial output file is
-// left behind. Phase timings print as the reference's "[TIMER]" lines.
+// process then exits with status 2 instead of 0; no partial output file is
+// left behind and an existing output is never truncated or removed (outputs
+// are renamed into place when complete, so the input may also be the output). Phase timings print as the reference's "[TIMER]" lines.
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -52,11 +53,6 @@ unsigned host_threads()
     return h ? h : 1;
 }
 
-bool is_gpu(Method m)
-{
-    return m == Method::FixedLength || m == Method::FixedLengthMulti || m == Method::RunLength;
-}
-
 size_t env_size(const char *name, size_t dflt)
 {
     const char *v = std::getenv(name);
@@ -85,6 +81,7 @@ bool fl_streamed(const Args &a, bool compress_op)
     return true;
 }
 
+// fl-cpu / rl-cpu: whole file in host memory, like the reference (main.cu:72-129).
 void compress(const Args &a)
 {
     if (fl_streamed(a, true))
@@ -92,21 +89,9 @@ void compress(const Args &a)
     Timer t;
     FileData in = loadFile(a.inputFile);
     t.done("Load data from file");
-    const bool rl = a.method == Method::RunLength || a.method == Method::RunLengthCPU;
     try {
-        if (!rl) {
-            flrl_fl_buf c{};
-            switch (a.method) {
-            case Method::FixedLength:
-                check(flrl_fl_compress(in.data, in.size, &c), "fl compress");
-                break;
-            case Method::FixedLengthMulti:
-                check(flrl_fl_compress_sharded(in.data, in.size, 0, &c), "fl sharded compress");
-                break;
-            default:
-                c = cpuCompressFL(in.data, in.size, host_threads());
-                break;
-            }
+        if (a.method == Method::FixedLengthCPU) {
+            flrl_fl_buf c = cpuCompressFL(in.data, in.size, host_threads());
             t.done("Compression");
             try {
                 saveCompressedFL(a.outputFile, c);
@@ -118,11 +103,7 @@ void compress(const Args &a)
             std::free(c.bits);
             std::free(c.values);
         } else {
-            flrl_rl_buf c{};
-            if (a.method == Method::RunLength)
-                check(flrl_rl_compress(in.data, in.size, &c), "rl compress");
-            else
-                c = cpuCompressRL(in.data, in.size);
+            flrl_rl_buf c = cpuCompressRL(in.data, in.size);
             t.done("Compression");
             try {
                 saveCompressedRL(a.outputFile, c);
@@ -142,23 +123,18 @@ void compress(const Args &a)
     std::free(in.data);
 }
 
+// fl-cpu / rl-cpu (main.cu:131-169).
 void decompress(const Args &a)
 {
     if (fl_streamed(a, false))
         return;
     Timer t;
     FileData out;
-    const bool rl = a.method == Method::RunLength || a.method == Method::RunLengthCPU;
-    if (!rl) {
+    if (a.method == Method::FixedLengthCPU) {
         flrl_fl_buf c = loadCompressedFL(a.inputFile);
         t.done("Load data from file");
         try {
-            if (is_gpu(a.method))
-                check(flrl_fl_decompress(c.input_size, c.bits, c.bits_size, c.values,
-                                         c.values_size, &out.data, &out.size),
-                      "fl decompress");
-            else
-                cpuDecompressFL(c, &out.data, &out.size, host_threads());
+            cpuDecompressFL(c, &out.data, &out.size, host_threads());
         } catch (...) {
             std::free(c.bits);
             std::free(c.values);
@@ -170,12 +146,7 @@ void decompress(const Args &a)
         flrl_rl_buf c = loadCompressedRL(a.inputFile);
         t.done("Load data from file");
         try {
-            if (is_gpu(a.method))
-                check(flrl_rl_decompress(c.input_size, c.counts, c.values, c.runs, &out.data,
-                                         &out.size),
-                      "rl decompress");
-            else
-                cpuDecompressRL(c, &out.data, &out.size);
+            cpuDecompressRL(c, &out.data, &out.size);
         } catch (...) {
             std::free(c.counts);
             std::free(c.values);
@@ -206,8 +177,10 @@ int main(int argc, char **argv)
         else
             decompress(a);
     } catch (const std::exception &e) {
+        // outputs are written to a temporary and renamed into place only on
+        // success (flrl_outfile.hpp), so there is nothing to clean up here: an
+        // existing output file is left as it was
         std::fprintf(stderr, "[ERROR]: %s\n", e.what());
-        std::remove(a.outputFile);
         return 2;
     }
     return 0;

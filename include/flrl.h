@@ -221,6 +221,11 @@ int flrl_time_next_kernel(void *start_event, void *stop_event);
  * 0 cancels. Never needed by callers. */
 int flrl_debug_skip_scratch_resets(int calls);
 
+/* Test hook: the streamed file paths (flrl_*_file) fail when a worker reaches
+ * chunk (or RL decode block) `chunk`, as a failed read or device call would.
+ * Process-wide; a negative value cancels. */
+int flrl_debug_fail_chunk(long long chunk);
+
 /* ---- RL, host buffers (synchronous) --------------------------------------- */
 int flrl_rl_compress(const uint8_t *data, size_t size, flrl_rl_buf *out);
 int flrl_rl_decompress(size_t output_size, const uint8_t *counts, const uint8_t *values,

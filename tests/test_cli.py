@@ -116,3 +116,51 @@ def test_gpu_methods_fail_loudly_without_device(cli_path, tmp_path, method):
     r = subprocess.run([cli_path, "c", method, str(src), str(out)], capture_output=True, text=True)
     assert r.returncode == 2 and "[ERROR]" in r.stderr
     assert not out.exists()
+
+
+@pytest.mark.parametrize("method", ["fl-cpu", "rl-cpu"])
+def test_failed_run_keeps_existing_output(cli_path, tmp_path, method):
+    """A run that fails (missing input, malformed input) leaves a pre-existing
+    output byte-for-byte alone and no temporary file behind."""
+    out = tmp_path / "old.out"
+    out.write_bytes(b"precious")
+    r = run(cli_path, "c", method, tmp_path / "missing.bin", out, check=False)
+    assert r.returncode == 2 and "[ERROR]:" in r.stderr
+    assert out.read_bytes() == b"precious"
+    (tmp_path / "bad").write_bytes(b"\x01\x02")  # truncated header
+    r = run(cli_path, "d", method, tmp_path / "bad", out, check=False)
+    assert r.returncode == 2
+    assert out.read_bytes() == b"precious"
+    assert sorted(p.name for p in tmp_path.iterdir()) == ["bad", "old.out"]
+
+
+@pytest.mark.parametrize("method", ["fl-cpu", "rl-cpu"])
+def test_input_may_be_output(cli_path, tmp_path, method):
+    """`compress c <m> f f` then `compress d <m> f f` restores f (the reference
+    loads the whole input before saving, so in == out works there too)."""
+    a = oracle.gen("lo4", 100_003, 5)
+    f = tmp_path / "f"
+    f.write_bytes(a.tobytes())
+    run(cli_path, "c", method, f, f)
+    if method == "fl-cpu":
+        assert f.read_bytes() == oracle.fl_file_bytes(a)
+    run(cli_path, "d", method, f, f)
+    assert f.read_bytes() == a.tobytes()
+    assert [p.name for p in tmp_path.iterdir()] == ["f"]
+
+
+def test_output_mode_follows_umask(cli_path, tmp_path):
+    import os
+    import stat
+    (tmp_path / "in").write_bytes(b"abc" * 100)
+    old = os.umask(0o027)
+    try:
+        run(cli_path, "c", "fl-cpu", tmp_path / "in", tmp_path / "o.fl")
+    finally:
+        os.umask(old)
+    assert stat.S_IMODE((tmp_path / "o.fl").stat().st_mode) == 0o640
+
+
+def test_output_to_dev_null(cli_path, tmp_path):
+    (tmp_path / "in").write_bytes(b"abc" * 100)
+    run(cli_path, "c", "fl-cpu", tmp_path / "in", "/dev/null")

@@ -260,3 +260,68 @@ def test_cli_rl_streamed(cli_path, tmp_path):
     r = subprocess.run([cli_path, "d", "rl", str(out), str(back)], env=env, capture_output=True, text=True)
     assert r.returncode == 0, r.stderr
     assert back.read_bytes() == data.tobytes()
+
+
+@pytest.mark.parametrize("op", ["fl_c", "fl_d", "rl_c", "rl_d"])
+@pytest.mark.parametrize("fail_at", [0, 5, 37])
+def test_injected_chunk_failure(tmp_path, op, fail_at):
+    """One pipeline fails (flrl_debug_fail_chunk) while the others and the
+    in-order writer are busy: the call raises, frees every pinned buffer only
+    after the writer has let go of it, and leaves an existing output alone."""
+    n = (48 << 20) + 99
+    data = _input("mixed", n, 4)
+    src, enc, out = tmp_path / "in", tmp_path / "enc", tmp_path / "out"
+    data.tofile(src)
+    chunk = 1 << 20
+    if op == "fl_d":
+        flrl.fl_compress_file(str(src), str(enc), 2, chunk)
+    elif op == "rl_d":
+        flrl.rl_compress_file(str(src), str(enc), 2, chunk)
+    out.write_bytes(b"keep me")
+    fn, arg = {"fl_c": (flrl.fl_compress_file, src), "fl_d": (flrl.fl_decompress_file, enc),
+               "rl_c": (flrl.rl_compress_file, src), "rl_d": (flrl.rl_decompress_file, enc)}[op]
+    flrl.debug_fail_chunk(fail_at)
+    try:
+        with pytest.raises(flrl.FLRLError) as e:
+            fn(str(arg), str(out), 4, chunk)
+        assert "injected" in str(e.value)
+    finally:
+        flrl.debug_fail_chunk(-1)
+    assert out.read_bytes() == b"keep me"
+    assert sorted(p.name for p in tmp_path.iterdir()) == sorted(
+        ["in", "out"] + (["enc"] if op.endswith("_d") else []))
+    fn(str(arg), str(out), 4, chunk)  # and the next call works
+    if op == "fl_c":
+        assert out.read_bytes() == _oracle_file(data)
+    elif op.endswith("_d"):
+        assert out.read_bytes() == data.tobytes()
+
+
+@pytest.mark.parametrize("method", ["fl", "fl-nccl", "rl"])
+def test_cli_streamed_in_place(cli_path, tmp_path, method):
+    """`compress c <m> f f` / `compress d <m> f f` (the streamed GPU paths read
+    the input while writing: the output goes to a temporary renamed into place)."""
+    data = _input("mixed", (3 << 20) + 11, 8)
+    f = tmp_path / "f"
+    f.write_bytes(data.tobytes())
+    env = dict(os.environ, FLRL_CHUNK_BYTES=str(1 << 20), FLRL_WORKERS="2")
+    for op in ("c", "d"):
+        r = subprocess.run([cli_path, op, method, str(f), str(f)], env=env, capture_output=True, text=True)
+        assert r.returncode == 0, r.stderr
+        if op == "c" and method != "rl":
+            assert f.read_bytes() == _oracle_file(data)
+    assert f.read_bytes() == data.tobytes()
+    assert [p.name for p in tmp_path.iterdir()] == ["f"]
+
+
+def test_cli_streamed_error_keeps_existing_output(cli_path, tmp_path):
+    bad = tmp_path / "bad.fl"
+    bad.write_bytes(struct.pack("<QQQ", 1000, 3, 5) + bytes(8))
+    out = tmp_path / "out"
+    out.write_bytes(b"old")
+    for argv in (["d", "fl", str(bad), str(out)], ["c", "fl", str(tmp_path / "missing"), str(out)],
+                 ["c", "rl", str(tmp_path / "missing"), str(out)]):
+        r = subprocess.run([cli_path, *argv], capture_output=True, text=True)
+        assert r.returncode == 2 and "[ERROR]" in r.stderr
+        assert out.read_bytes() == b"old"
+    assert sorted(p.name for p in tmp_path.iterdir()) == ["bad.fl", "out"]
