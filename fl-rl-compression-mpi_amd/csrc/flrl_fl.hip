@@ -733,48 +733,8 @@ extern "C" int flrl_fl_compress(const uint8_t *data, size_t size, flrl_fl_buf *o
         return FLRL_OK;
     if (flrl_device_count() <= 0)
         return set_error(FLRL_E_NODEV, "flrl_fl_compress: no HIP device visible");
-    const size_t frames = div_up(size, kFrame);
-    const size_t in_b = round_up(size, 16), bits_b = round_up(frames, 16);
-    const size_t val_b = flrl_fl_values_capacity(size), scr_b = flrl_fl_scratch_bytes(size);
-    DevBuf dev;
-    if (dev.alloc(in_b + bits_b + val_b + 16 + scr_b) != hipSuccess)
-        return set_error(FLRL_E_NOMEM, "Cannot allocate memory (device, %zu bytes)",
-                         in_b + bits_b + val_b + 16 + scr_b);
-    uint8_t *d_in = dev.as<uint8_t>(0);
-    uint8_t *d_bits = dev.as<uint8_t>(in_b);
-    uint8_t *d_values = dev.as<uint8_t>(in_b + bits_b);
-    uint64_t *d_vsize = dev.as<uint64_t>(in_b + bits_b + val_b);
-    void *d_scr = dev.as<void>(in_b + bits_b + val_b + 16);
-    FLRL_HIP(hipMemcpy(d_in, data, size, hipMemcpyHostToDevice));
-    int rc = flrl_fl_encode_device(d_in, size, d_bits, d_values, d_vsize, d_scr, scr_b, nullptr);
-    if (rc)
-        return rc;
-    uint64_t vsize = 0;
-    FLRL_HIP(hipMemcpy(&vsize, d_vsize, sizeof(vsize), hipMemcpyDeviceToHost));
-    const int kerr = flrl_scratch_error(d_scr, nullptr);
-    if (kerr)
-        return set_error(kerr, "flrl_fl_compress: device error %d", kerr);
-    uint8_t *h_bits = static_cast<uint8_t *>(malloc(frames));
-    uint8_t *h_vals = static_cast<uint8_t *>(malloc(vsize ? vsize : 1));
-    if (!h_bits || !h_vals) {
-        free(h_bits);
-        free(h_vals);
-        return set_error(FLRL_E_NOMEM, "Cannot allocate memory");
-    }
-    hipError_t e1 = hipMemcpy(h_bits, d_bits, frames, hipMemcpyDeviceToHost);
-    hipError_t e2 = hipMemcpy(h_vals, d_values, vsize, hipMemcpyDeviceToHost);
-    if (e1 != hipSuccess || e2 != hipSuccess) {
-        free(h_bits);
-        free(h_vals);
-        return set_error(FLRL_E_HIP, "flrl_fl_compress: copy-out failed: %s",
-                         hipGetErrorString(e1 != hipSuccess ? e1 : e2));
-    }
-    out->bits = h_bits;
-    out->bits_size = frames;
-    out->values = h_vals;
-    out->values_size = vsize;
-    out->input_size = size;
-    return FLRL_OK;
+    // pinned, chunked, two chunks in flight per pipeline (flrl_stream.hip)
+    return fl_compress_host(data, size, out);
 }
 
 extern "C" int flrl_fl_decompress(size_t output_size, const uint8_t *bits, size_t bits_size,
@@ -793,53 +753,13 @@ extern "C" int flrl_fl_decompress(size_t output_size, const uint8_t *bits, size_
     if (flrl_device_count() <= 0)
         return set_error(FLRL_E_NODEV, "flrl_fl_decompress: no HIP device visible");
     // Format hardening: the reference reads out of
-    // bounds on any of these; the output for valid files is unchanged.
+    // bounds on these; the output for valid input is unchanged. Widths and
+    // valuesSize are checked in the pipeline's chunk-offset pass.
     if (bits_size != div_up(output_size, kFrame))
         return set_error(FLRL_E_FORMAT, "bitsSize %zu != ceil(inputSize %zu / 128)", bits_size,
                          output_size);
-    uint64_t sum_full = 0;
-    for (size_t f = 0; f < bits_size; ++f) {
-        if (bits[f] < 1 || bits[f] > 8)
-            return set_error(FLRL_E_FORMAT, "frame %zu has width %u (must be 1..8)", f,
-                             (unsigned)bits[f]);
-        if (f + 1 < bits_size)
-            sum_full += bits[f];
-    }
-    const uint64_t cnt_last = output_size - (bits_size - 1) * (uint64_t)kFrame;
-    const uint64_t expect = 16 * sum_full + (cnt_last * bits[bits_size - 1] + 7) / 8;
-    if (expect != values_size)
-        return set_error(FLRL_E_FORMAT, "valuesSize %zu != %llu implied by the widths",
-                         values_size, (unsigned long long)expect);
-
-    const size_t bits_b = round_up(bits_size, 16), val_b = round_up(values_size, 16);
-    const size_t out_b = round_up(output_size, 16), scr_b = flrl_fl_scratch_bytes(output_size);
-    DevBuf dev;
-    if (dev.alloc(bits_b + val_b + out_b + scr_b) != hipSuccess)
-        return set_error(FLRL_E_NOMEM, "Cannot allocate memory (device, %zu bytes)",
-                         bits_b + val_b + out_b + scr_b);
-    uint8_t *d_bits = dev.as<uint8_t>(0);
-    uint8_t *d_vals = dev.as<uint8_t>(bits_b);
-    uint8_t *d_out = dev.as<uint8_t>(bits_b + val_b);
-    void *d_scr = dev.as<void>(bits_b + val_b + out_b);
-    FLRL_HIP(hipMemcpy(d_bits, bits, bits_size, hipMemcpyHostToDevice));
-    FLRL_HIP(hipMemcpy(d_vals, values, values_size, hipMemcpyHostToDevice));
-    int rc = flrl_fl_decode_device(d_bits, bits_size, d_vals, values_size, d_out, output_size,
-                                   d_scr, scr_b, nullptr);
-    if (rc)
-        return rc;
-    const int kerr = flrl_scratch_error(d_scr, nullptr);
-    if (kerr)
-        return set_error(kerr, "flrl_fl_decompress: device error %d", kerr);
-    uint8_t *h = static_cast<uint8_t *>(malloc(output_size));
-    if (!h)
-        return set_error(FLRL_E_NOMEM, "Cannot allocate memory");
-    hipError_t e = hipMemcpy(h, d_out, output_size, hipMemcpyDeviceToHost);
-    if (e != hipSuccess) {
-        free(h);
-        return set_error(FLRL_E_HIP, "flrl_fl_decompress: copy-out failed: %s",
-                         hipGetErrorString(e));
-    }
-    *out = h;
-    *out_size = output_size;
-    return FLRL_OK;
+    const int rc = fl_decompress_host(output_size, bits, bits_size, values, values_size, out);
+    if (rc == FLRL_OK)
+        *out_size = output_size;
+    return rc;
 }

@@ -28,6 +28,10 @@ hipError_t scratch_reset(void *p, size_t bytes, hipStream_t s);
 // flrl_debug_fail_chunk: true when the streamed file paths should fail chunk c.
 bool debug_fail_chunk(size_t c);
 
+// Host-buffer FL through the pinned chunk pipelines (flrl_stream.hip).
+int fl_compress_host(const uint8_t *data, size_t size, flrl_fl_buf *out);
+int fl_decompress_host(size_t n, const uint8_t *bits, size_t F, const uint8_t *values, size_t V, uint8_t **out);
+
 void kernel_timing_begin(hipStream_t s);
 void kernel_timing_end(hipStream_t s);
 

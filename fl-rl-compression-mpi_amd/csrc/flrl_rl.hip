@@ -42,28 +42,26 @@
 #include "flrl_device.hpp"
 #include "flrl_internal.hpp"
 
-// Phase-timing hooks for scripts/ubench_rl.hip (no-ops in the library).
-#ifndef FLRL_RL_PHASE
-#define FLRL_RL_PHASE_BEGIN() ((void)0)
-#define FLRL_RL_PHASE(k) ((void)0)
-#define FLRL_RL_PHASE_END() ((void)0)
-#endif
-// Per-tile timestamp hooks for scripts/ubench_rl.hip -DTRACE (no-ops here).
-// Extra dynamic LDS per encode workgroup (occupancy experiments only).
-#ifndef FLRL_RL_DYN_LDS
-#define FLRL_RL_DYN_LDS 0
-#endif
-#ifndef FLRL_RL_TRACE
-#define FLRL_RL_TRACE(tile, k) ((void)0)
+// Timing ablations of rl_encode_wave_kernel (scripts/ubench_rl.hip only; the
+// output is wrong with any of them): 1 no look-back, 2 no record stores, 4 no
+// run staging in the scan pass, 8 no head masks / scans (data only touched).
+#ifndef FLRL_RL_ABL
+#define FLRL_RL_ABL 0
 #endif
 
 namespace flrl {
 
-constexpr int kRlThreads = 256;                     // encode workgroup: 4 waves, 3 per CU
-constexpr int kRlLaneBytes = 128;                   // contiguous bytes per lane
-constexpr int kRlSub = 4;                           // sub-tiles per tile (one look-back each tile)
-constexpr int kRlTileBytes = kRlLaneBytes * kRlThreads * kRlSub;  // 4 x 32 KiB sub-tiles through LDS
-constexpr int kRlLookG = 1;      // look-back granules per lane (window 64 G tiles)
+#ifndef FLRL_RL_LB
+#define FLRL_RL_LB 64
+#endif
+constexpr int kRlThreads = 256;                     // encode workgroup: 4 waves (LB 64: 94 VGPRs, 32 KiB LDS, 5 per CU)
+constexpr int kRlLaneBytes = FLRL_RL_LB;            // contiguous bytes per lane (64 or 128)
+constexpr int kRlSub = 32768 / (64 * kRlLaneBytes); // sub-chunks per wave chunk (one look-back per tile)
+constexpr int kRlTileBytes = kRlLaneBytes * kRlThreads * kRlSub;  // 128 KiB: 4 waves x 32 KiB
+#ifndef FLRL_RL_LOOKG
+#define FLRL_RL_LOOKG 1
+#endif
+constexpr int kRlLookG = FLRL_RL_LOOKG;  // look-back granules per lane (window 64 G tiles)
 constexpr int kRlStageBytes = 16256;  // LDS run staging (48 KiB of LDS per workgroup)
 
 constexpr int kRdRuns = 4096;        // runs per decode tile
@@ -298,455 +296,22 @@ __device__ __forceinline__ uint64_t lookback_seg(uint64_t *status, uint32_t tile
     }
 }
 
-// One tile of SUB sub-tiles per workgroup, in ticket order; a sub-tile is
-// T/64 waves x 64 lanes x LB bytes and sits in LDS (LDS-DMA, 1 KiB per
-// wave-instruction, coalesced), swizzled so that every lane then reads ITS OWN
-// contiguous LB bytes conflict-free: row r keeps chunk c at r*LB + ((c^(r&7))*16).
-// Per lane: natural-head masks, count, first/last natural head. LB < 255, so a
-// lane holds at most one split head, and only before its first natural head.
-// Two 32-bit wave scans per sub-tile: PhaseMaps (lane states relative to the
-// tile's incoming state) and the count of heads that do not depend on that
-// state (all heads from the tile's first natural head on), whose runs are
-// staged in LDS at their tile-local index while the sub-tiles stream through.
-// The tile's composite map then goes through ONE look-back (one per SUB
-// sub-tiles); the c_in-dependent prefix (split heads before the first natural
-// head, and the count of the run that head ends) is written after it and the
-// staged records leave contiguously. A tile with more state-independent runs
-// than the staging area holds (dense data) re-reads its sub-tiles after the
-// look-back and emits per wave.
-template <int T, int LB, int SUB>
-__global__ __launch_bounds__(T) void rl_encode_kernel(
-    const uint8_t *__restrict__ in, uint64_t n, uint32_t ntiles, uint8_t *__restrict__ counts,
-    uint8_t *__restrict__ values, uint64_t *__restrict__ runs_out, Ctrl *ctrl, uint64_t *status)
-{
-    constexpr int W = T / kWave;
-    constexpr int CH = LB / 16;  // 16-byte chunks per lane
-    constexpr int WB = kWave * LB;
-    constexpr int TB = WB * W;   // sub-tile bytes
-    constexpr int SW = kRlStageBytes / W / 2;  // per-wave staged records (dense path)
-    constexpr int SC = kRlStageBytes / 2;      // tile staging: runs
-    static_assert(LB == 128, "the swizzle and the 2 x u64 head masks assume 8 chunks per lane");
-    // ONE LDS object: [sub-tile image][staging: counts | values][small]
-    __shared__ __attribute__((aligned(16))) uint8_t s_lds[TB + kRlStageBytes + 128];
-    uint8_t *const img = s_lds;
-    uint8_t *const tsc = s_lds + TB;
-    uint8_t *const tsv = tsc + SC;
-    uint8_t *const stc = s_lds + TB + (size_t)(threadIdx.x / kWave) * 2 * SW;
-    uint8_t *const stv = stc + SW;
-    uint32_t *const s_wmap = reinterpret_cast<uint32_t *>(s_lds + TB + kRlStageBytes);
-    uint32_t *const s_wfirst = s_wmap + W;
-    uint32_t *const s_wh = s_wfirst + W;
-    uint32_t *const s_ticket = s_wh + W;
-    uint64_t *const s_state = reinterpret_cast<uint64_t *>(s_lds + TB + kRlStageBytes + 120);
-    static_assert(3 * W * 4 + 4 <= 120, "small LDS fields");
-
-    const int tid = threadIdx.x;
-    const int lane = tid & (kWave - 1);
-    const int w = tid / kWave;
-    const uint32_t row = (uint32_t)tid;  // lane row within a sub-tile
-    const uint32_t o = row * LB;          // its byte offset in the sub-tile
-    const uint8_t *my = img + o;
-    FLRL_RL_PHASE_BEGIN();
-    const uint32_t tile = take_ticket(ctrl, s_ticket);
-    if (tile >= ntiles) {  // the scratch's ticket was not reset for this launch
-        if (threadIdx.x == 0)
-            raise_error(ctrl, FLRL_E_ARG);
-        return;
-    }
-    FLRL_RL_TRACE(tile, 0);
-    const uint64_t tile_off = (uint64_t)tile * (SUB * TB);
-    const uint32_t tile_len = (uint32_t)(n - tile_off < (uint64_t)(SUB * TB) ? n - tile_off : SUB * TB);
-
-    // ---- one sub-tile into LDS, natural heads, lane/wave/tile phase scans ---
-    struct Sub {
-        uint32_t nat[CH / 2];  // 16-bit masks, two per word
-        uint32_t ncnt, fpos, lpos, vbl, p0;
-        uint32_t lrel;   // lane start state from the sub-tile's start (PhaseMap)
-        uint32_t smap;   // the sub-tile's PhaseMap
-        uint32_t sfirst; // first natural head in the sub-tile (0xFFFFFFFF: none)
-        uint64_t off;    // sub-tile offset in the input
-    };
-    constexpr int NJ = WB / 1024;  // 1 KiB wave-loads per sub-tile
-    const uint32_t swz_c = ((uint32_t)lane & 7u) ^ (((uint32_t)lane >> 3) & 7u);
-    // sub-tile s of this tile into registers, placed as the LDS-DMA places it
-    auto prefetch = [&](int s, u32x4 (&pf)[NJ]) {
-        const uint64_t wave_off = tile_off + (uint64_t)s * TB + (uint64_t)w * WB;
-        if (wave_off + WB <= n) {
-#pragma unroll
-            for (int j = 0; j < NJ; ++j)
-                pf[j] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(
-                    in + wave_off + (uint32_t)(j * 8 + lane / 8) * LB + swz_c * 16));
-        } else {
-#pragma unroll
-            for (int j = 0; j < NJ; ++j)
-                pf[j] = load16_tail(in, wave_off + (uint32_t)(j * 8 + lane / 8) * LB + swz_c * 16, n);
-        }
-    };
-    // use_pf: the sub-tile is in pf (prefetched during the previous scan), else
-    // it comes by LDS-DMA; pf_next: prefetch sub-tile s+1 once this one is in LDS
-    auto scan_sub = [&](int s, Sub &L, u32x4 (&pf)[NJ], bool use_pf, bool pf_next) {
-        L.off = tile_off + (uint64_t)s * TB;
-        const uint64_t wave_off = L.off + (uint64_t)w * WB;
-        {
-            uint8_t *dst = img + w * WB;
-            if (use_pf) {
-#pragma unroll
-                for (int j = 0; j < NJ; ++j)
-                    *reinterpret_cast<u32x4 *>(dst + j * 1024 + lane * 16) = pf[j];
-            } else if (wave_off + WB <= n) {
-#pragma unroll
-                for (int j = 0; j < NJ; ++j) {
-                    const uint8_t *src = in + wave_off + (uint32_t)(j * 8 + lane / 8) * LB + swz_c * 16;
-                    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)src,
-                                                     (__attribute__((address_space(3))) void *)(dst + j * 1024),
-                                                     16, 0, 0);
-                }
-            } else {
-#pragma unroll
-                for (int j = 0; j < NJ; ++j) {
-                    const uint64_t g = wave_off + (uint32_t)(j * 8 + lane / 8) * LB + swz_c * 16;
-                    *reinterpret_cast<u32x4 *>(dst + j * 1024 + lane * 16) = load16_tail(in, g, n);
-                }
-            }
-        }
-        const uint64_t lane_off = L.off + o;
-        L.vbl = lane_off >= n ? 0u : (n - lane_off >= LB ? (uint32_t)LB : (uint32_t)(n - lane_off));
-        const uint32_t pstart = (tid == 0 && L.off > 0) ? in[L.off - 1] : 0u;
-        __syncthreads();  // waits for the LDS-DMA too
-        FLRL_RL_TRACE(tile, s == 0 ? 1 : (s == SUB - 1 ? 2 : 7));  // 7: scratch slot
-        if (pf_next)
-            prefetch(s + 1, pf);  // lands while this sub-tile is scanned
-        L.p0 = row == 0 ? pstart : img[(row - 1) * LB + ((7u ^ ((row - 1) & 7u)) * 16) + 15];
-        {
-            uint32_t p = L.p0;
-            const bool full = L.off + TB <= n;  // tile-uniform: no per-chunk length masks
-#pragma unroll
-            for (int c = 0; c < CH; ++c) {
-                const u32x4 x = *reinterpret_cast<const u32x4 *>(my + ((c ^ (row & 7u)) * 16));
-                uint32_t m = nat_mask(x, p);
-                if (!full) {
-                    const uint32_t vb = L.vbl > 16u * c ? (L.vbl - 16u * c >= 16 ? 16u : L.vbl - 16u * c) : 0u;
-                    m &= vb >= 16 ? 0xFFFFu : ((1u << vb) - 1u);
-                }
-                if (c & 1)
-                    L.nat[c / 2] |= m << 16;
-                else
-                    L.nat[c / 2] = m;
-                p = x.w >> 24;
-            }
-            if (lane_off == 0)
-                L.nat[0] |= 1u;  // byte 0 is a head
-            const uint64_t a = ((uint64_t)L.nat[1] << 32) | L.nat[0], b = ((uint64_t)L.nat[3] << 32) | L.nat[2];
-            L.ncnt = (uint32_t)(__popcll(a) + __popcll(b));
-            L.fpos = a ? (uint32_t)__builtin_ctzll(a) : (b ? 64u + (uint32_t)__builtin_ctzll(b) : (uint32_t)LB);
-            L.lpos = b ? 127u - (uint32_t)__builtin_clzll(b) : (a ? 63u - (uint32_t)__builtin_clzll(a) : 0u);
-        }
-        const bool has = L.ncnt != 0;
-        const uint32_t lmap = has ? pm_make(true, L.vbl - L.lpos) : pm_make(false, L.vbl);
-        const uint32_t incl = wave_incl_scan_map(lmap);
-        uint32_t lexcl = __shfl_up(incl, 1, kWave);
-        lexcl = lane == 0 ? kMapIdent : lexcl;
-        {
-            const unsigned long long hb = __ballot(has);
-            const int fl = hb ? __ffsll(hb) - 1 : 0;
-            const uint32_t ff = (uint32_t)__shfl(L.fpos, fl, kWave);
-            if (lane == kWave - 1)
-                s_wmap[w] = incl;
-            if (lane == 0)
-                s_wfirst[w] = hb ? (uint32_t)(w * WB + fl * LB) + ff : 0xFFFFFFFFu;
-        }
-        __syncthreads();
-        uint32_t smap = kMapIdent, wave_pre = kMapIdent, sfirst = 0xFFFFFFFFu;
-#pragma unroll
-        for (int v = 0; v < W; ++v) {
-            if (v == w)
-                wave_pre = smap;
-            smap = pm_compose(smap, s_wmap[v]);
-            if (sfirst == 0xFFFFFFFFu && s_wfirst[v] != 0xFFFFFFFFu)
-                sfirst = s_wfirst[v];
-        }
-        L.smap = smap;
-        L.sfirst = sfirst;
-        L.lrel = pm_compose(wave_pre, lexcl);
-    };
-    // lane head masks, given the lane's start state c0 and whether a split
-    // before its first natural head counts
-    auto head_masks = [&](const Sub &L, uint32_t c0, bool with_split, uint64_t &h0, uint64_t &h1) {
-        const uint32_t j0 = c0 == 0 ? 0u : 255u - c0;
-        const bool split = with_split && j0 < L.fpos && j0 < L.vbl;
-        h0 = h1 = 0;
-#pragma unroll
-        for (int c = 0; c < CH; ++c) {
-            uint32_t h = (L.nat[c / 2] >> (16 * (c & 1))) & 0xFFFFu;
-            if (split && (j0 >> 4) == (uint32_t)c)
-                h |= 1u << (j0 & 15u);
-            if (c < 4)
-                h0 |= (uint64_t)h << (16 * c);
-            else
-                h1 |= (uint64_t)h << (16 * (c - 4));
-        }
-    };
-    // a lane's runs in order from head masks: count = distance to the previous
-    // head (the lane's first: c_first + pos), value = the byte before the head.
-    // No natural head lies strictly between two heads, so that byte equals the
-    // byte AT the previous head (the lane's first run: the byte before the
-    // lane, p0): it is read one iteration ahead, off the loop's critical path.
-    auto lane_runs = [&](const Sub &L, uint64_t h0, uint64_t h1, uint32_t c_first, uint8_t *sc, uint8_t *sv,
-                         uint32_t slot) {
-        int prev = -1;
-        uint32_t val = L.p0;
-        while (h0 | h1) {
-            int pos;
-            if (h0) {
-                pos = __builtin_ctzll(h0);
-                h0 &= h0 - 1;
-            } else {
-                pos = 64 + __builtin_ctzll(h1);
-                h1 &= h1 - 1;
-            }
-            uint32_t cnt = prev < 0 ? add_c(c_first, (uint32_t)pos) : (uint32_t)(pos - prev);
-            cnt = cnt == 0 ? 255u : cnt;
-            const uint32_t q = (uint32_t)pos;
-            const uint32_t nval = my[(((q >> 4) ^ (row & 7u)) * 16) + (q & 15u)];  // the next run's value
-            sc[slot] = (uint8_t)cnt;
-            sv[slot] = (uint8_t)val;
-            val = nval;
-            ++slot;
-            prev = pos;
-        }
-    };
-
-    // ---- sub-tiles: stage the state-independent runs ------------------------
-    // Runs are staged while they fit; from the first sub-tile that overflows the
-    // staging area on (nst), sub-tiles are re-read after the look-back instead.
-    u32x4 pf[NJ];                      // the next sub-tile, in flight during a scan
-    uint32_t rel_in = kMapIdent;       // PhaseMap from the tile start to this sub-tile
-    uint32_t first = 0xFFFFFFFFu;      // the tile's first natural head (tile-relative)
-    uint32_t K = 0;                    // state-independent heads so far
-    int nst = SUB;                     // sub-tiles whose runs are all staged
-    uint32_t Kst = 0, rel_st = kMapIdent;  // K and rel_in at sub-tile nst
-    uint8_t v0 = 0;                    // the tile's first byte
-    for (int s = 0; s < SUB; ++s) {
-        if (tile_off + (uint64_t)s * TB >= n)
-            break;  // tile-uniform
-        if (s > 0)
-            __syncthreads();  // the previous sub-tile's LDS readers are done
-        Sub L;
-        scan_sub(s, L, pf, s > 0, s + 1 < SUB && tile_off + (uint64_t)(s + 1) * TB < n);
-        if (s == 0)
-            v0 = img[0];
-        const bool seen = first != 0xFFFFFFFFu;  // a natural head before this sub-tile
-        const uint32_t lrel = pm_compose(rel_in, L.lrel);
-        uint32_t indep = 0;
-        bool lane_indep = false, after = false;
-        if (seen) {
-            lane_indep = after = true;
-        } else if (L.sfirst != 0xFFFFFFFFu && o + LB > L.sfirst) {
-            lane_indep = true;
-            after = o > L.sfirst;
-        }
-        const uint32_t cr = after ? pm_apply(lrel, 1) : 0u;  // constant after the first head
-        uint64_t h0 = 0, h1 = 0;
-        if (lane_indep) {
-            head_masks(L, cr, after, h0, h1);
-            indep = (uint32_t)(__popcll(h0) + __popcll(h1));
-        }
-        const uint32_t hincl = wave_incl_scan_u32(indep);
-        if (lane == kWave - 1)
-            s_wh[w] = hincl;
-        __syncthreads();
-        uint32_t ks = 0, wave_hbase = 0;
-#pragma unroll
-        for (int v = 0; v < W; ++v) {
-            wave_hbase += v < w ? s_wh[v] : 0u;
-            ks += s_wh[v];
-        }
-        if (nst == SUB && K + ks > (uint32_t)SC) {  // tile-uniform
-            nst = s;
-            Kst = K;
-            rel_st = rel_in;
-        }
-        const bool stage = nst == SUB;
-        const uint32_t slot = K + wave_hbase + (hincl - indep);
-        if (!seen && L.sfirst != 0xFFFFFFFFu)
-            first = (uint32_t)s * TB + L.sfirst;
-        K += ks;
-        rel_in = pm_compose(rel_in, L.smap);
-        if (w == 0 && (s + 1 == SUB || tile_off + (uint64_t)(s + 1) * TB >= n)) {
-            // the tile's map is complete: publish it before staging the last runs
-            publish_seg(status, tile, first != 0xFFFFFFFFu ? sm_nat(first, K, rel_in & 0xFFu) : sm_nonat(tile_len));
-            FLRL_RL_TRACE(tile, 3);
-        }
-        if (stage && indep)
-            lane_runs(L, h0, h1, cr, tsc, tsv, slot);
-    }
-    const int ns = (int)((tile_len + TB - 1) / TB);  // sub-tiles in this tile
-    if (nst >= ns) {
-        nst = ns;
-        Kst = K;
-        rel_st = rel_in;
-    }
-    const uint32_t pre = first != 0xFFFFFFFFu ? first : tile_len;
-    FLRL_RL_PHASE(1);
-
-    // ---- one look-back: (heads before the tile, chunk state at its start) --
-    if (w == 0) {
-        const uint64_t tmap = first != 0xFFFFFFFFu ? sm_nat(first, K, rel_in & 0xFFu) : sm_nonat(tile_len);
-#ifdef FLRL_RL_NO_LOOKBACK  // timing ablation only (scripts/ubench_rl.hip): wrong output
-        const uint64_t state = (((uint64_t)tile * 4000ull) << 8) | 1u;
-        (void)tmap;
-#else
-        const uint64_t state = lookback_seg<kRlLookG>(status, tile, tmap, ctrl);
-#endif
-        FLRL_RL_TRACE(tile, 4);
-        if (lane == 0)
-            *s_state = state;
-    }
-    __syncthreads();
-    FLRL_RL_PHASE(2);
-    const uint64_t h_in = sm_h(*s_state);
-    const uint32_t c_in = sm_c(*s_state);
-    const uint32_t S = splits(c_in, pre);  // split heads before the first natural head
-    {
-        // staged sub-tiles [0, nst): split heads h_in + j end full 255-byte
-        // chunks of the tile's first byte, then the staged records
-        const uint32_t st_len = (uint32_t)nst * TB;
-        const uint32_t S_st = splits(c_in, pre < st_len ? pre : st_len);
-        for (uint32_t j = (uint32_t)tid; j < S_st; j += T) {
-            const uint64_t gi = h_in + j;
-            if (gi > 0) {
-                counts[gi - 1] = 255;
-                values[gi - 1] = v0;
-            }
-        }
-        const uint64_t g0 = h_in + S_st;  // global index of the first natural head
-        if (Kst) {
-            if (tid == 0 && g0 > 0) {
-                const uint32_t c = add_c(c_in, first);
-                counts[g0 - 1] = (uint8_t)(c == 0 ? 255u : c);
-                values[g0 - 1] = tsv[0];
-            }
-#ifndef FLRL_RL_NO_EMIT  // timing ablation only (scripts/ubench_rl.hip): wrong output
-            for (uint32_t j = 1 + (uint32_t)tid; j < Kst; j += T) {
-                counts[g0 + j - 1] = tsc[j];
-                values[g0 + j - 1] = tsv[j];
-            }
-#endif
-        }
-    }
-    if (nst < ns) {
-        // sub-tiles [nst, ns): re-read and emit with the true states
-        uint32_t rel = rel_st;
-        uint64_t hb = h_in + splits(c_in, pre < (uint32_t)nst * TB ? pre : (uint32_t)nst * TB) + Kst;
-        for (int s = nst; s < ns; ++s) {
-            __syncthreads();  // staging and image readers are done
-            Sub L;
-            scan_sub(s, L, pf, s > nst, s + 1 < ns);
-            const uint32_t c_lane = pm_apply(pm_compose(rel, L.lrel), c_in);
-            uint64_t hm0, hm1;
-            head_masks(L, c_lane, true, hm0, hm1);
-            const uint32_t hl = (uint32_t)(__popcll(hm0) + __popcll(hm1));
-            const uint32_t hincl = wave_incl_scan_u32(hl);
-            if (lane == kWave - 1)
-                s_wh[w] = hincl;
-            __syncthreads();
-            uint32_t hs = 0, wave_hbase = 0;
-#pragma unroll
-            for (int v = 0; v < W; ++v) {
-                wave_hbase += v < w ? s_wh[v] : 0u;
-                hs += s_wh[v];
-            }
-            uint64_t g = hb + wave_hbase + (hincl - hl);
-            const uint32_t wave_heads = (uint32_t)wave_sum_u64((uint64_t)hl);
-            if (wave_heads <= (uint32_t)SW) {
-                // sparse wave: stage at (g - first g of the wave), store contiguously
-                const uint64_t gw = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(g >> 32), 0) << 32) |
-                                    (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)g, 0);
-                lane_runs(L, hm0, hm1, c_lane, stc, stv, (uint32_t)(g - gw));
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                for (uint32_t j = lane; j < wave_heads; j += kWave) {
-                    const uint64_t gi = gw + j;
-                    if (gi > 0) {
-                        counts[gi - 1] = stc[j];
-                        values[gi - 1] = stv[j];
-                    }
-                }
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            } else {
-                // dense wave: ONE lane row at a time, lane t taking byte positions
-                // t and 64 + t of the row (ranks by popcount): contiguous stores
-                const uint64_t below = ((uint64_t)1 << lane) - 1;
-#pragma unroll 1
-                for (int r = 0; r < kWave; ++r) {
-                    const uint64_t h0 = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(hm0 >> 32), r) << 32) |
-                                        (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)hm0, r);
-                    const uint64_t h1 = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(hm1 >> 32), r) << 32) |
-                                        (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)hm1, r);
-                    const uint64_t g_row = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(g >> 32), r) << 32) |
-                                           (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)g, r);
-                    const uint32_t c_row = (uint32_t)__builtin_amdgcn_readlane((int)c_lane, r);
-                    const uint32_t p_row = (uint32_t)__builtin_amdgcn_readlane((int)L.p0, r);
-                    const uint32_t rr = (uint32_t)(w * kWave + r);
-                    const uint8_t *rowp = img + rr * LB;
-#pragma unroll
-                    for (int half = 0; half < 2; ++half) {
-                        const uint64_t hm = half ? h1 : h0;
-                        if ((hm >> lane) & 1u) {
-                            const uint64_t bl = hm & below;
-                            const uint32_t pos = (uint32_t)(half * 64 + lane);
-                            const uint32_t rank = (half ? (uint32_t)__popcll(h0) : 0u) + (uint32_t)__popcll(bl);
-                            int prev;
-                            if (bl)
-                                prev = half * 64 + 63 - __builtin_clzll(bl);
-                            else
-                                prev = (half && h0) ? 63 - __builtin_clzll(h0) : -1;
-                            uint32_t cnt = prev < 0 ? add_c(c_row, pos) : pos - (uint32_t)prev;
-                            cnt = cnt == 0 ? 255u : cnt;
-                            const uint32_t q = pos - 1;
-                            const uint32_t val = pos == 0 ? p_row : rowp[(((q >> 4) ^ (rr & 7u)) * 16) + (q & 15u)];
-                            const uint64_t gi = g_row + rank;
-                            if (gi > 0) {
-                                counts[gi - 1] = (uint8_t)cnt;
-                                values[gi - 1] = (uint8_t)val;
-                            }
-                        }
-                    }
-                }
-            }
-            hb += hs;
-            rel = pm_compose(rel, L.smap);
-        }
-    }
-    FLRL_RL_PHASE(3);
-    FLRL_RL_PHASE_END();
-    FLRL_RL_TRACE(tile, 5);
-
-    // ---- the final run (ends at byte n-1) ----------------------------------
-    if (tile + 1 == ntiles && tid == 0) {
-        const uint64_t R = h_in + S + K;
-        const uint32_t c_end = pm_apply(rel_in, c_in);
-        counts[R - 1] = (uint8_t)(c_end == 0 ? 255u : c_end);
-        values[R - 1] = in[n - 1];
-        *runs_out = R;
-    }
-}
-
-// Wave-private variant. The tile is the same 128 KiB, but wave w owns its w-th
-// contiguous 32 KiB chunk and streams it as SUB sub-chunks of 8 KiB through its
-// OWN 8 KiB of LDS (registers -> ds_write -> each lane reads its 128 contiguous
-// bytes; LDS ops of one wave are in order, so no barrier), with the next
-// sub-chunk's loads in flight during each scan. All scans are wave scans with
+// RL encode. A tile is 128 KiB taken by ticket; wave w owns its w-th
+// contiguous 32 KiB chunk and streams it as SUB sub-chunks of 64*LB bytes
+// through its OWN slice of LDS (registers -> ds_write -> each lane reads its LB
+// contiguous bytes; LDS ops of one wave are in order, so no barrier), with the
+// next sub-chunk's loads in flight during each scan. The image is swizzled so
+// that those lane reads are bank-conflict free: row r keeps its 16-byte chunk c
+// at r*LB + ((c ^ swz(r)) * 16). LB < 255, so a lane holds at most one split
+// head, before its first natural head. All scans are wave scans with
 // the carries (PhaseMap, first natural head, state-independent head count) in
 // uniform registers, and each wave stages its own state-independent runs, so a
 // tile has three block barriers (ticket, wave maps, state) instead of four per
 // sub-tile. The wave maps compose (sm_compose) into the tile's map for the one
 // look-back; the resolved state is then advanced wave by wave, and every wave
 // emits its own prefix (split heads before its first natural head), staged runs
-// and, past a staging overflow, re-read sub-chunks (as rl_encode_kernel).
+// and, past a staging overflow, re-read sub-chunks: sparse ones through the
+// staging area, dense ones one lane row at a time (contiguous stores).
 template <int T, int LB, int SUB>
 __global__ __launch_bounds__(T) void rl_encode_wave_kernel(
     const uint8_t *__restrict__ in, uint64_t n, uint32_t ntiles, uint8_t *__restrict__ counts,
@@ -760,7 +325,7 @@ __global__ __launch_bounds__(T) void rl_encode_wave_kernel(
     constexpr int SW = kRlStageBytes / W / 2;  // staged records per wave
     constexpr int NJ = WB / 1024;    // 1 KiB wave-loads per sub-chunk
     constexpr uint32_t kNone = 0xFFFFFFFFu;
-    static_assert(LB == 128, "the swizzle and the 2 x u64 head masks assume 8 chunks per lane");
+    static_assert(LB == 128 || LB == 64, "one or two u64 head masks per lane");
     static_assert(TBT == kRlTileBytes, "tile geometry shared with the layout");
     __shared__ __attribute__((aligned(16))) uint8_t s_lds[W * WB + kRlStageBytes];
     __shared__ uint64_t s_map[W];
@@ -776,6 +341,10 @@ __global__ __launch_bounds__(T) void rl_encode_wave_kernel(
     const uint32_t row = (uint32_t)lane;
     const uint32_t o = row * LB;
     const uint8_t *my = img + o;
+    // swizzle of row r: its chunk c sits at position c ^ swz(r); 16 lanes of a
+    // ds_read_b128 (rows r..r+15, one chunk each) then cover all 64 banks
+    auto swz = [](uint32_t r) -> uint32_t { return LB == 128 ? (r & 7u) : ((r >> 2) & 3u); };
+    const uint32_t sw = swz(row);
 
     const uint32_t tile = take_ticket(ctrl, &s_ticket);
     if (tile >= ntiles) {  // the scratch's ticket was not reset for this launch
@@ -786,25 +355,29 @@ __global__ __launch_bounds__(T) void rl_encode_wave_kernel(
     const uint64_t chunk_off = (uint64_t)tile * TBT + (uint64_t)w * CB;
     const uint32_t chunk_len = chunk_off >= n ? 0u : (n - chunk_off < (uint64_t)CB ? (uint32_t)(n - chunk_off) : (uint32_t)CB);
     const int ns = (int)((chunk_len + WB - 1) / WB);  // sub-chunks of this wave
-    const uint32_t swz_c = ((uint32_t)lane & 7u) ^ (((uint32_t)lane >> 3) & 7u);
+    // LDS slot (j, lane) = byte j*1024 + lane*16 = row j*RPL + lane/CH, position
+    // lane % CH; swz(row) depends on lane/CH only, as RPL is a multiple of 8 (LB
+    // 128) or 16 (LB 64)
+    constexpr int RPL = 1024 / LB;  // rows per wave-load
+    const uint32_t swz_c = ((uint32_t)lane % CH) ^ swz((uint32_t)lane / CH);
 
-    // sub-chunk s into registers, placed as the LDS image wants it: row r keeps
-    // chunk c at r*LB + ((c ^ (r & 7)) * 16), each wave-load 1 KiB contiguous
+    // sub-chunk s into registers, placed as the LDS image wants it, each
+    // wave-load 1 KiB of LDS
     auto load_sub = [&](int s, u32x4 (&pf)[NJ]) {
         const uint64_t so = chunk_off + (uint64_t)s * WB;
         if (so + WB <= n) {
 #pragma unroll
             for (int j = 0; j < NJ; ++j)
                 pf[j] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(
-                    in + so + (uint32_t)(j * 8 + lane / 8) * LB + swz_c * 16));
+                    in + so + (uint32_t)(j * RPL + lane / CH) * LB + swz_c * 16));
         } else {
 #pragma unroll
             for (int j = 0; j < NJ; ++j)
-                pf[j] = load16_tail(in, so + (uint32_t)(j * 8 + lane / 8) * LB + swz_c * 16, n);
+                pf[j] = load16_tail(in, so + (uint32_t)(j * RPL + lane / CH) * LB + swz_c * 16, n);
         }
     };
     struct Sub {
-        uint32_t nat[CH / 2];  // 16-bit masks, two per word
+        uint32_t nat[CH / 2];  // 16-bit masks, two per word (CH >= 4)
         uint32_t ncnt, fpos, lpos, vbl, p0;
         uint32_t lrel;    // lane start state from the sub-chunk's start (PhaseMap)
         uint32_t smap;    // the sub-chunk's PhaseMap
@@ -825,8 +398,26 @@ __global__ __launch_bounds__(T) void rl_encode_wave_kernel(
         u32x4 x[CH];
 #pragma unroll
         for (int c = 0; c < CH; ++c)
-            x[c] = *reinterpret_cast<const u32x4 *>(my + ((c ^ (row & 7u)) * 16));
+            x[c] = *reinterpret_cast<const u32x4 *>(my + ((c ^ sw) * 16));
         const uint32_t mylast = x[CH - 1].w >> 24;
+        if (FLRL_RL_ABL & 8) {
+            uint32_t acc = 0;
+#pragma unroll
+            for (int c = 0; c < CH; ++c)
+                acc ^= x[c].x ^ x[c].y ^ x[c].z ^ x[c].w;
+            L.p0 = p_sub;
+#pragma unroll
+            for (int q = 0; q < CH / 2; ++q)
+                L.nat[q] = q == 0 ? (acc & 1u) : 0u;
+            L.ncnt = acc & 1u;
+            L.fpos = 0;
+            L.lpos = 0;
+            L.vbl = LB;
+            L.lrel = kMapIdent;
+            L.smap = kMapIdent;
+            L.sfirst = acc & 1u ? 0u : kNone;
+            return mylast;
+        }
         const uint32_t up = (uint32_t)__shfl_up((int)mylast, 1, kWave);
         L.p0 = lane == 0 ? p_sub : up;
         {
@@ -847,7 +438,10 @@ __global__ __launch_bounds__(T) void rl_encode_wave_kernel(
             }
             if (lane_off == 0)
                 L.nat[0] |= 1u;  // byte 0 is a head
-            const uint64_t a = ((uint64_t)L.nat[1] << 32) | L.nat[0], b = ((uint64_t)L.nat[3] << 32) | L.nat[2];
+            const uint64_t a = ((uint64_t)L.nat[1] << 32) | L.nat[0];
+            uint64_t b = 0;
+            if constexpr (CH == 8)
+                b = ((uint64_t)L.nat[3] << 32) | L.nat[2];
             L.ncnt = (uint32_t)(__popcll(a) + __popcll(b));
             L.fpos = a ? (uint32_t)__builtin_ctzll(a) : (b ? 64u + (uint32_t)__builtin_ctzll(b) : (uint32_t)LB);
             L.lpos = b ? 127u - (uint32_t)__builtin_clzll(b) : (a ? 63u - (uint32_t)__builtin_clzll(a) : 0u);
@@ -879,7 +473,9 @@ __global__ __launch_bounds__(T) void rl_encode_wave_kernel(
                 h1 |= (uint64_t)h << (16 * (c - 4));
         }
     };
-    // a lane's runs from its head masks (see rl_encode_kernel::lane_runs)
+    // a lane's runs from its head masks: head h ends the run before it (count =
+    // h - previous head, or c_first + h for the lane's first head, 255 for 0;
+    // value = the byte before h), records at slot, slot + 1, ...
     auto lane_runs = [&](const Sub &L, uint64_t h0, uint64_t h1, uint32_t c_first, uint8_t *sc, uint8_t *sv,
                          uint32_t slot) {
         int prev = -1;
@@ -896,7 +492,7 @@ __global__ __launch_bounds__(T) void rl_encode_wave_kernel(
             uint32_t cnt = prev < 0 ? add_c(c_first, (uint32_t)pos) : (uint32_t)(pos - prev);
             cnt = cnt == 0 ? 255u : cnt;
             const uint32_t q = (uint32_t)pos;
-            const uint32_t nval = my[(((q >> 4) ^ (row & 7u)) * 16) + (q & 15u)];
+            const uint32_t nval = my[(((q >> 4) ^ sw) * 16) + (q & 15u)];
             sc[slot] = (uint8_t)cnt;
             sv[slot] = (uint8_t)val;
             val = nval;
@@ -951,7 +547,7 @@ __global__ __launch_bounds__(T) void rl_encode_wave_kernel(
             first = (uint32_t)s * WB + L.sfirst;
         K += ks;
         rel_in = pm_compose(rel_in, L.smap);
-        if (nst == SUB && indep)
+        if (nst == SUB && indep && !(FLRL_RL_ABL & 4))
             lane_runs(L, h0, h1, cr, stc, stv, slot);
     }
     if (nst >= ns) {
@@ -970,8 +566,13 @@ __global__ __launch_bounds__(T) void rl_encode_wave_kernel(
 #pragma unroll
         for (int v = 1; v < W; ++v)
             tmap = sm_compose(tmap, s_map[v]);
-        publish_seg(status, tile, tmap);
-        uint64_t st = lookback_seg<kRlLookG>(status, tile, tmap, ctrl);
+        uint64_t st;
+        if (FLRL_RL_ABL & 1) {
+            st = sm_const((uint64_t)tile * 4096u, 0);
+        } else {
+            publish_seg(status, tile, tmap);
+            st = lookback_seg<kRlLookG>(status, tile, tmap, ctrl);
+        }
         if (lane == 0) {
 #pragma unroll
             for (int v = 0; v < W; ++v) {
@@ -981,7 +582,7 @@ __global__ __launch_bounds__(T) void rl_encode_wave_kernel(
         }
     }
     __syncthreads();
-    if (ns == 0)
+    if (ns == 0 || (FLRL_RL_ABL & 2))
         return;
     const uint64_t h_in = sm_h(s_st[w]);
     const uint32_t c_in = sm_c(s_st[w]);
@@ -1062,7 +663,7 @@ __global__ __launch_bounds__(T) void rl_encode_wave_kernel(
                     const uint32_t rr = (uint32_t)r;
                     const uint8_t *rowp = img + rr * LB;
 #pragma unroll
-                    for (int half = 0; half < 2; ++half) {
+                    for (int half = 0; half < CH / 4; ++half) {
                         const uint64_t hm = half ? h1 : h0;
                         if ((hm >> lane) & 1u) {
                             const uint64_t bl = hm & below;
@@ -1076,7 +677,7 @@ __global__ __launch_bounds__(T) void rl_encode_wave_kernel(
                             uint32_t cnt = prev < 0 ? add_c(c_row, pos) : pos - (uint32_t)prev;
                             cnt = cnt == 0 ? 255u : cnt;
                             const uint32_t q = pos - 1;
-                            const uint32_t val = pos == 0 ? p_row : rowp[(((q >> 4) ^ (rr & 7u)) * 16) + (q & 15u)];
+                            const uint32_t val = pos == 0 ? p_row : rowp[(((q >> 4) ^ swz(rr)) * 16) + (q & 15u)];
                             const uint64_t gi = g_row + rank;
                             if (gi > 0) {
                                 counts[gi - 1] = (uint8_t)cnt;
@@ -1514,20 +1115,10 @@ extern "C" int flrl_rl_encode_device(const uint8_t *d_in, size_t n, uint8_t *d_c
         return set_error(FLRL_E_ARG, "flrl_rl_encode_device: input too large");
     Ctrl *ctrl = static_cast<Ctrl *>(d_scratch);
     uint64_t *status = reinterpret_cast<uint64_t *>(ctrl + 1);
-#ifdef FLRL_RL_ENCODE_V1  // A/B builds only (scripts/ab_libs.py)
-    constexpr bool v1 = true;
-#else
-    constexpr bool v1 = false;
-#endif
     kernel_timing_begin(s);
-    if (v1)
-        hipLaunchKernelGGL((rl_encode_kernel<kRlThreads, kRlLaneBytes, kRlSub>), dim3((uint32_t)L.tiles),
-                           dim3(kRlThreads), FLRL_RL_DYN_LDS, s, d_in, (uint64_t)n, (uint32_t)L.tiles, d_counts,
-                           d_values, d_runs, ctrl, status);
-    else
-        hipLaunchKernelGGL((rl_encode_wave_kernel<kRlThreads, kRlLaneBytes, kRlSub>), dim3((uint32_t)L.tiles),
-                           dim3(kRlThreads), 0, s, d_in, (uint64_t)n, (uint32_t)L.tiles, d_counts, d_values,
-                           d_runs, ctrl, status);
+    hipLaunchKernelGGL((rl_encode_wave_kernel<kRlThreads, kRlLaneBytes, kRlSub>), dim3((uint32_t)L.tiles),
+                       dim3(kRlThreads), 0, s, d_in, (uint64_t)n, (uint32_t)L.tiles, d_counts, d_values,
+                       d_runs, ctrl, status);
     kernel_timing_end(s);
     FLRL_HIP(hipGetLastError());
     return FLRL_OK;

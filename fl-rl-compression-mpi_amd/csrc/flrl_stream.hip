@@ -27,11 +27,13 @@
 #include <stdint.h>
 #include <stdio.h>
 #include <string.h>
+#include <sys/mman.h>
 #include <sys/stat.h>
 #include <unistd.h>
 
 #include <atomic>
 #include <condition_variable>
+#include <map>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -153,8 +155,11 @@ struct Slot {
 
 struct Slots {
     Slot slot[2];
+    int dev = -1;  // owning device (set before alloc when freed from another thread)
     ~Slots()
     {
+        if (dev >= 0)
+            (void)hipSetDevice(dev);
         for (Slot &x : slot) {
             if (x.s)
                 (void)hipStreamSynchronize(x.s);
@@ -221,6 +226,556 @@ void release_unwritten(std::mutex &m, std::condition_variable &cv, std::vector<R
 
 using namespace flrl;
 
+namespace flrl {
+namespace {
+
+// ---- FL pipelines over any source / sink -----------------------------------
+// Byte sources and sinks of the FL pipelines. Compress reads the raw input and
+// writes the container's two arrays; decompress reads the container's arrays
+// and writes the raw output. File forms use pread/pwrite (container at its
+// on-disk offsets), memory forms memcpy (the flrl_fl_compress/_decompress host
+// API). Every call is made by a worker thread on a disjoint range.
+// `direct` (memory forms only): the pipelines copy between the caller's
+// pageable memory and HBM with hipMemcpyAsync instead of memcpy through the
+// pinned staging; ptr()/wptr() give the addresses.
+struct FdRaw {  // raw bytes of a file
+    int fd;
+    bool direct = false;
+    const uint8_t *ptr(uint64_t) const { return nullptr; }
+    uint8_t *wptr(uint64_t) const { return nullptr; }
+    bool read(void *d, size_t len, uint64_t off) { return pread_all(fd, d, len, off); }
+    bool write(const void *p, size_t len, uint64_t off) { return pwrite_all(fd, p, len, off); }
+};
+struct MemRawIn {
+    const uint8_t *p;
+    bool direct = false;
+    const uint8_t *ptr(uint64_t off) const { return p + off; }
+    bool read(void *d, size_t len, uint64_t off)
+    {
+        memcpy(d, p + off, len);
+        return true;
+    }
+};
+struct MemRawOut {
+    uint8_t *p;
+    bool direct = false;
+    uint8_t *wptr(uint64_t off) const { return p + off; }
+    bool write(const void *q, size_t len, uint64_t off)
+    {
+        memcpy(p + off, q, len);
+        return true;
+    }
+};
+struct FdFl {  // FL container file: u64 header[3] | bits[F] | values[V]
+    int fd;
+    uint64_t F;
+    bool direct = false;
+    const uint8_t *bits_ptr(uint64_t) const { return nullptr; }
+    const uint8_t *values_ptr(uint64_t) const { return nullptr; }
+    uint8_t *bits_wptr(uint64_t) const { return nullptr; }
+    uint8_t *values_wptr(uint64_t) const { return nullptr; }
+    bool read_bits(void *d, size_t len, uint64_t f) { return pread_all(fd, d, len, kHeader + f); }
+    bool read_values(void *d, size_t len, uint64_t v) { return pread_all(fd, d, len, kHeader + F + v); }
+    bool write_bits(const void *q, size_t len, uint64_t f) { return pwrite_all(fd, q, len, kHeader + f); }
+    bool write_values(const void *q, size_t len, uint64_t v) { return pwrite_all(fd, q, len, kHeader + F + v); }
+};
+struct MemFl {  // FL arrays in host memory
+    const uint8_t *rbits = nullptr, *rvalues = nullptr;
+    uint8_t *wbits = nullptr, *wvalues = nullptr;
+    bool direct = false;
+    const uint8_t *bits_ptr(uint64_t f) const { return rbits + f; }
+    const uint8_t *values_ptr(uint64_t v) const { return rvalues + v; }
+    uint8_t *bits_wptr(uint64_t f) const { return wbits + f; }
+    uint8_t *values_wptr(uint64_t v) const { return wvalues + v; }
+    bool read_bits(void *d, size_t len, uint64_t f)
+    {
+        memcpy(d, rbits + f, len);
+        return true;
+    }
+    bool read_values(void *d, size_t len, uint64_t v)
+    {
+        memcpy(d, rvalues + v, len);
+        return true;
+    }
+    bool write_bits(const void *q, size_t len, uint64_t f)
+    {
+        memcpy(wbits + f, q, len);
+        return true;
+    }
+    bool write_values(const void *q, size_t len, uint64_t v)
+    {
+        memcpy(wvalues + v, q, len);
+        return true;
+    }
+};
+
+// Pinned staging + device buffers of one pipeline, kept across calls: a
+// pipeline's hipHostMalloc/hipMalloc of 2 x ~2 chunks costs more than a
+// 16 MiB chunk's transfer. At most kPoolCap idle sets are kept per shape.
+constexpr size_t kPoolCap = 8;
+struct PoolKey {
+    int dev;
+    size_t a, b, c, scr;
+    bool operator<(const PoolKey &o) const
+    {
+        if (dev != o.dev)
+            return dev < o.dev;
+        if (a != o.a)
+            return a < o.a;
+        if (b != o.b)
+            return b < o.b;
+        if (c != o.c)
+            return c < o.c;
+        return scr < o.scr;
+    }
+};
+std::mutex g_pool_m;
+std::map<PoolKey, std::vector<Slots *>> g_pool;
+
+Slots *slots_acquire(int dev, size_t a, size_t b, size_t c, size_t scr)
+{
+    {
+        std::lock_guard<std::mutex> g(g_pool_m);
+        auto it = g_pool.find(PoolKey{dev, a, b, c, scr});
+        if (it != g_pool.end() && !it->second.empty()) {
+            Slots *x = it->second.back();
+            it->second.pop_back();
+            return x;
+        }
+    }
+    Slots *x = new Slots;
+    x->dev = dev;
+    if (x->alloc(a, b, c, scr) != hipSuccess) {
+        delete x;
+        return nullptr;
+    }
+    return x;
+}
+
+void slots_release(Slots *x, size_t a, size_t b, size_t c, size_t scr)
+{
+    if (!x)
+        return;
+    for (Slot &y : x->slot)  // idle: nothing of a previous call still in flight
+        (void)hipStreamSynchronize(y.s);
+    {
+        std::lock_guard<std::mutex> g(g_pool_m);
+        std::vector<Slots *> &v = g_pool[PoolKey{x->dev, a, b, c, scr}];
+        if (v.size() < kPoolCap) {
+            v.push_back(x);
+            return;
+        }
+    }
+    delete x;
+}
+
+struct SlotsLease {
+    Slots *x = nullptr;
+    size_t a = 0, b = 0, c = 0, scr = 0;
+    SlotsLease(int dev, size_t a_, size_t b_, size_t c_, size_t s_) : a(a_), b(b_), c(c_), scr(s_)
+    {
+        x = slots_acquire(dev, a, b, c, scr);
+    }
+    ~SlotsLease() { slots_release(x, a, b, c, scr); }
+};
+
+// FL compress of n bytes from `src` into `dst`, frame-aligned chunks through
+// W pipelines (pipeline w on devs[w % devs.size()], two chunks in flight).
+// Bits land at frame c*chunk/128; a chunk's values at the sum of the earlier
+// chunks' sizes, which each pipeline learns from the chunk before its own (a
+// chain of u64s, no writer thread): every pipeline writes its own bytes, so
+// host copies (memcpy or pwrite) run W-wide and a pipeline's buffers are never
+// read by another thread. *V_total = valuesSize.
+template <class Src, class Dst>
+int fl_compress_core(Src &src, Dst &dst, uint64_t n, const std::vector<int> &devs, int W, size_t chunk,
+                     uint64_t *V_total, const char *who)
+{
+    const size_t cf = chunk / kFrame;
+    const size_t nchunks = n ? (size_t)((n + chunk - 1) / chunk) : 0;
+    *V_total = 0;
+    if (!nchunks)
+        return FLRL_OK;
+    Failure fail;
+    std::mutex m;
+    std::condition_variable cv;
+    fail.wait_m = &m;
+    fail.wait_cv = &cv;
+    std::vector<uint64_t> voff(nchunks + 1, 0);
+    std::vector<char> known(nchunks + 1, 0);  // under m
+    known[0] = 1;
+    const int nw = pipelines(W, nchunks);
+    const size_t scr_b = flrl_fl_scratch_bytes(chunk), vcap = flrl_fl_values_capacity(chunk);
+
+    auto worker = [&](int w) {
+        const int dev = devs[(size_t)w % devs.size()];
+        if (hipSetDevice(dev) != hipSuccess) {
+            fail.set(FLRL_E_HIP, "hipSetDevice failed");
+            return;
+        }
+        SlotsLease lease(dev, chunk, cf, vcap, scr_b);
+        if (!lease.x) {
+            fail.set(FLRL_E_NOMEM, "Cannot allocate memory (pinned staging)");
+            return;
+        }
+        Slots &S = *lease.x;
+        auto finish = [&](size_t c, int k) -> bool {  // chunk c in slot k: check, place
+            Slot &x = S.slot[k];
+            if (hipStreamSynchronize(x.s) != hipSuccess) {
+                fail.set(FLRL_E_HIP, "fl encode: stream failed");
+                return false;
+            }
+            const int kerr = flrl_scratch_error(x.d_scr, x.s);
+            if (kerr) {
+                fail.set(kerr, "fl encode: device error");
+                return false;
+            }
+            const uint64_t len = (c + 1 == nchunks) ? n - (uint64_t)c * chunk : chunk;
+            const size_t fb = (size_t)((len + kFrame - 1) / kFrame);
+            const size_t vb = (size_t)x.h_u64[0];
+            if (vb > vcap) {
+                fail.set(FLRL_E_HIP, "fl encode: values size out of range");
+                return false;
+            }
+            if (!dst.direct && hipMemcpyAsync(x.h_c, x.d_c, vb, hipMemcpyDeviceToHost, x.s) != hipSuccess) {
+                fail.set(FLRL_E_HIP, "fl encode: copy-out failed");
+                return false;
+            }
+            uint64_t vo;
+            {  // this chunk's values offset, then the next chunk's
+                std::unique_lock<std::mutex> g(m);
+                cv.wait(g, [&] { return known[c] || fail.failed.load(); });
+                if (!known[c])
+                    return false;
+                vo = voff[c];
+                voff[c + 1] = vo + vb;
+                known[c + 1] = 1;
+            }
+            cv.notify_all();
+            if (dst.direct) {
+                if ((vb && hipMemcpyAsync(dst.values_wptr(vo), x.d_c, vb, hipMemcpyDeviceToHost, x.s) != hipSuccess) ||
+                    hipStreamSynchronize(x.s) != hipSuccess) {
+                    fail.set(FLRL_E_HIP, "fl encode: copy-out failed");
+                    return false;
+                }
+                return true;
+            }
+            if (hipStreamSynchronize(x.s) != hipSuccess) {
+                fail.set(FLRL_E_HIP, "fl encode: copy-out failed");
+                return false;
+            }
+            if (!dst.write_bits(x.h_b, fb, (uint64_t)c * cf) || !dst.write_values(x.h_c, vb, vo)) {
+                fail.set(FLRL_E_ARG, "[FileIO] Cannot write to file");
+                return false;
+            }
+            return true;
+        };
+        size_t pend = SIZE_MAX;  // chunk in flight in slot pend_k
+        int pend_k = 0;
+        int i = 0;
+        for (size_t c = (size_t)w; c < nchunks && !fail.failed.load(); c += (size_t)nw, ++i) {
+            const int k = i & 1;  // slot k last held chunk c - 2*nw, finished an iteration ago
+            Slot &x = S.slot[k];
+            const uint64_t off = (uint64_t)c * chunk;
+            const size_t len = (size_t)((c + 1 == nchunks) ? n - off : chunk);
+            const size_t fb = (len + kFrame - 1) / kFrame;
+            if (debug_fail_chunk(c)) {
+                fail.set(FLRL_E_HIP, "injected failure (flrl_debug_fail_chunk)");
+                break;
+            }
+            if (!src.direct && !src.read(x.h_a, len, off)) {
+                fail.set(FLRL_E_ARG, "[FileIO] Cannot read file content");
+                break;
+            }
+            uint8_t *bits_to = dst.direct ? dst.bits_wptr((uint64_t)c * cf) : x.h_b;
+            if (hipMemcpyAsync(x.d_a, src.direct ? src.ptr(off) : x.h_a, len, hipMemcpyHostToDevice, x.s) != hipSuccess ||
+                flrl_fl_encode_device(x.d_a, len, x.d_b, x.d_c, x.d_u64, x.d_scr, x.scr_bytes, x.s) != FLRL_OK ||
+                hipMemcpyAsync(x.h_u64, x.d_u64, 8, hipMemcpyDeviceToHost, x.s) != hipSuccess ||
+                hipMemcpyAsync(bits_to, x.d_b, fb, hipMemcpyDeviceToHost, x.s) != hipSuccess) {
+                fail.set(FLRL_E_HIP, std::string("fl encode: ") + flrl_last_error());
+                break;
+            }
+            if (pend != SIZE_MAX && !finish(pend, pend_k))
+                break;
+            pend = c;
+            pend_k = k;
+        }
+        if (!fail.failed.load() && pend != SIZE_MAX)
+            (void)finish(pend, pend_k);
+    };
+    std::vector<std::thread> threads;
+    for (int w = 0; w < nw; ++w)
+        threads.emplace_back(worker, w);
+    for (auto &t : threads)
+        t.join();
+    if (fail.failed.load())
+        return set_error(fail.code ? fail.code : FLRL_E_HIP, "%s: %s", who, fail.msg.c_str());
+    *V_total = voff[nchunks];
+    return FLRL_OK;
+}
+
+// Value offset of every chunk (16 x the widths of all earlier frames) in one
+// pass over the widths, 4 MiB at a time, validating them (1..8) and the
+// values size they imply. voff has nchunks + 1 entries.
+template <class Src>
+int fl_chunk_offsets(Src &src, uint64_t n, uint64_t F, uint64_t V, size_t chunk, std::vector<uint64_t> &voff)
+{
+    const size_t cf = chunk / kFrame;
+    const size_t nchunks = (size_t)((n + chunk - 1) / chunk);
+    voff.assign(nchunks + 1, 0);
+    std::vector<uint8_t> win(4u << 20);
+    uint64_t acc = 0;  // width units before the current window's chunk
+    uint8_t last_w = 0;
+    for (size_t c = 0; c < nchunks; ++c) {
+        voff[c] = 16 * acc;
+        const uint64_t f0 = (uint64_t)c * cf, f1 = f0 + cf < F ? f0 + cf : F;
+        for (uint64_t f = f0; f < f1;) {
+            const size_t k = (size_t)(f1 - f < win.size() ? f1 - f : win.size());
+            if (!src.read_bits(win.data(), k, f))
+                return set_error(FLRL_E_ARG, "[FileIO] Cannot read file content");
+            uint32_t bad = 0;
+            uint64_t s = 0;
+            for (size_t i = 0; i < k; ++i) {  // vectorised: sum and range check
+                const uint8_t b = win[i];
+                bad |= (uint8_t)(b - 1) > 7u;
+                s += b;
+            }
+            if (bad) {
+                for (size_t i = 0; i < k; ++i)
+                    if ((uint8_t)(win[i] - 1) > 7u)
+                        return set_error(FLRL_E_FORMAT, "frame %llu has width %u (must be 1..8)",
+                                         (unsigned long long)(f + i), (unsigned)win[i]);
+            }
+            acc += s;
+            last_w = win[k - 1];
+            f += k;
+        }
+    }
+    // the last frame holds cnt_last bytes: (cnt_last * b + 7) / 8 of its 16 b
+    const uint64_t cnt_last = n - (F - 1) * kFrame;
+    const uint64_t expect = 16 * (acc - last_w) + (cnt_last * last_w + 7) / 8;
+    if (expect != V)
+        return set_error(FLRL_E_FORMAT, "valuesSize %llu != %llu implied by the widths",
+                         (unsigned long long)V, (unsigned long long)expect);
+    voff[nchunks] = V;
+    return FLRL_OK;
+}
+
+// FL decompress of n bytes: each chunk's widths and values read by its
+// pipeline, decoded, written at its output offset.
+template <class Src, class Dst>
+int fl_decompress_core(Src &src, Dst &dst, uint64_t n, uint64_t F, uint64_t V, const std::vector<int> &devs,
+                       int W, size_t chunk, const char *who)
+{
+    const size_t cf = chunk / kFrame;
+    const size_t nchunks = (size_t)((n + chunk - 1) / chunk);
+    std::vector<uint64_t> voff;
+    int rc = fl_chunk_offsets(src, n, F, V, chunk, voff);
+    if (rc)
+        return rc;
+    Failure fail;
+    const int nw = pipelines(W, nchunks);
+    const size_t vcap = flrl_fl_values_capacity(chunk), scr_b = flrl_fl_scratch_bytes(chunk);
+    auto worker = [&](int w) {
+        const int dev = devs[(size_t)w % devs.size()];
+        if (hipSetDevice(dev) != hipSuccess) {
+            fail.set(FLRL_E_HIP, "hipSetDevice failed");
+            return;
+        }
+        SlotsLease lease(dev, cf, vcap, chunk, scr_b);
+        if (!lease.x) {
+            fail.set(FLRL_E_NOMEM, "Cannot allocate memory (pinned staging)");
+            return;
+        }
+        Slots &S = *lease.x;
+        auto finish = [&](size_t c, int k) -> bool {  // wait, check, write chunk c
+            Slot &x = S.slot[k];
+            if (hipStreamSynchronize(x.s) != hipSuccess) {
+                fail.set(FLRL_E_HIP, "fl decode: stream failed");
+                return false;
+            }
+            const int kerr = flrl_scratch_error(x.d_scr, x.s);
+            if (kerr) {
+                fail.set(kerr, "fl decode: malformed data (widths or valuesSize)");
+                return false;
+            }
+            const uint64_t off = (uint64_t)c * chunk;
+            const size_t len = (size_t)((c + 1 == nchunks) ? n - off : chunk);
+            if (!dst.direct && !dst.write(x.h_c, len, off)) {
+                fail.set(FLRL_E_ARG, "[FileIO] Cannot write to file");
+                return false;
+            }
+            return true;
+        };
+        size_t pend = SIZE_MAX;
+        int pend_k = 0;
+        int i = 0;
+        for (size_t c = (size_t)w; c < nchunks && !fail.failed.load(); c += (size_t)nw, ++i) {
+            const int k = i & 1;
+            Slot &x = S.slot[k];
+            // slot k last held chunk c - 2*nw, finished (written) in the previous iteration
+            const uint64_t off = (uint64_t)c * chunk;
+            const size_t len = (size_t)((c + 1 == nchunks) ? n - off : chunk);
+            const size_t fb = (len + kFrame - 1) / kFrame;
+            const uint64_t vo = voff[c], vb = voff[c + 1] - voff[c];
+            if (vb > vcap || voff[c + 1] < voff[c]) {
+                fail.set(FLRL_E_FORMAT, "valuesSize larger than the widths imply");
+                break;
+            }
+            if (debug_fail_chunk(c)) {
+                fail.set(FLRL_E_HIP, "injected failure (flrl_debug_fail_chunk)");
+                break;
+            }
+            if (!src.direct &&
+                (!src.read_bits(x.h_a, fb, (uint64_t)c * cf) || !src.read_values(x.h_b, (size_t)vb, vo))) {
+                fail.set(FLRL_E_ARG, "[FileIO] Cannot read file content");
+                break;
+            }
+            if (hipMemcpyAsync(x.d_a, src.direct ? src.bits_ptr((uint64_t)c * cf) : x.h_a, fb, hipMemcpyHostToDevice,
+                               x.s) != hipSuccess ||
+                (vb && hipMemcpyAsync(x.d_b, src.direct ? src.values_ptr(vo) : x.h_b, (size_t)vb,
+                                      hipMemcpyHostToDevice, x.s) != hipSuccess) ||
+                flrl_fl_decode_device(x.d_a, fb, x.d_b, (size_t)vb, x.d_c, len, x.d_scr, x.scr_bytes, x.s) !=
+                    FLRL_OK ||
+                hipMemcpyAsync(dst.direct ? dst.wptr(off) : x.h_c, x.d_c, len, hipMemcpyDeviceToHost, x.s) !=
+                    hipSuccess) {
+                fail.set(FLRL_E_HIP, std::string("fl decode: ") + flrl_last_error());
+                break;
+            }
+            if (pend != SIZE_MAX && !finish(pend, pend_k))
+                break;
+            pend = c;
+            pend_k = k;
+        }
+        if (!fail.failed.load() && pend != SIZE_MAX)
+            (void)finish(pend, pend_k);
+    };
+    std::vector<std::thread> threads;
+    for (int w = 0; w < nw; ++w)
+        threads.emplace_back(worker, w);
+    for (auto &t : threads)
+        t.join();
+    if (fail.failed.load())
+        return set_error(fail.code ? fail.code : FLRL_E_HIP, "%s: %s", who, fail.msg.c_str());
+    return FLRL_OK;
+}
+
+std::vector<int> all_devices(int ndev)
+{
+    std::vector<int> d((size_t)ndev);
+    for (int i = 0; i < ndev; ++i)
+        d[(size_t)i] = i;
+    return d;
+}
+
+}  // namespace
+
+// Host-buffer FL (flrl_fl_compress / flrl_fl_decompress, flrl_fl.hip): the
+// same pipelines memory to memory on the current device, kHostWorkers wide
+// (host memcpy into pinned staging is the per-pipeline limit, not PCIe).
+constexpr int kHostWorkers = 4;
+constexpr size_t kHostChunk = 16ull << 20;
+struct HostCfg {
+    int workers = kHostWorkers;
+    size_t chunk = kHostChunk;
+    bool direct = false;
+    HostCfg()
+    {  // A/B overrides (scripts/bench_stream.py)
+        if (const char *v = getenv("FLRL_HOST_WORKERS"))
+            workers = atoi(v) > 0 ? atoi(v) : workers;
+        if (const char *v = getenv("FLRL_HOST_CHUNK"))
+            chunk = strtoull(v, nullptr, 0) >= kFrame ? chunk_size(strtoull(v, nullptr, 0)) : chunk;
+        if (const char *v = getenv("FLRL_HOST_DIRECT"))
+            direct = atoi(v) != 0;
+    }
+};
+
+// malloc for a large host output, backed by transparent huge pages where the
+// kernel allows (madvise before the first touch): the first touch of freshly
+// mapped 4 KiB pages, not PCIe, bounds the host-buffer API otherwise.
+uint8_t *host_alloc(size_t bytes)
+{
+    uint8_t *p = static_cast<uint8_t *>(malloc(bytes ? bytes : 1));
+    if (p && bytes >= (8u << 20) && getenv("FLRL_HOST_THP") && atoi(getenv("FLRL_HOST_THP"))) {
+        const uintptr_t a = ((uintptr_t)p + (2u << 20) - 1) & ~(uintptr_t)((2u << 20) - 1);
+        const uintptr_t e = ((uintptr_t)p + bytes) & ~(uintptr_t)((2u << 20) - 1);
+        if (e > a)
+            (void)madvise(reinterpret_cast<void *>(a), e - a, MADV_HUGEPAGE);
+    }
+    return p;
+}
+
+int fl_compress_host(const uint8_t *data, size_t size, flrl_fl_buf *out)
+{
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess)
+        return set_error(FLRL_E_NODEV, "flrl_fl_compress: no HIP device visible");
+    const size_t F = (size + kFrame - 1) / kFrame;
+    uint8_t *bits = host_alloc(F);
+    uint8_t *vals = host_alloc(size);  // V <= n; shrunk below
+    if (!bits || !vals) {
+        free(bits);
+        free(vals);
+        return set_error(FLRL_E_NOMEM, "Cannot allocate memory");
+    }
+    const HostCfg cfg;
+    MemRawIn src{data};
+    src.direct = cfg.direct;
+    MemFl dst;
+    dst.wbits = bits;
+    dst.wvalues = vals;
+    dst.direct = cfg.direct;
+    uint64_t V = 0;
+    const int rc = fl_compress_core(src, dst, size, std::vector<int>{dev}, cfg.workers, cfg.chunk, &V,
+                                    "flrl_fl_compress");
+    (void)hipSetDevice(dev);
+    if (rc) {
+        free(bits);
+        free(vals);
+        return rc;
+    }
+    if (V < size) {
+        uint8_t *v2 = static_cast<uint8_t *>(realloc(vals, V ? V : 1));
+        if (v2)
+            vals = v2;
+    }
+    out->bits = bits;
+    out->bits_size = F;
+    out->values = vals;
+    out->values_size = V;
+    out->input_size = size;
+    return FLRL_OK;
+}
+
+int fl_decompress_host(size_t n, const uint8_t *bits, size_t F, const uint8_t *values, size_t V, uint8_t **out)
+{
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess)
+        return set_error(FLRL_E_NODEV, "flrl_fl_decompress: no HIP device visible");
+    uint8_t *h = host_alloc(n);
+    if (!h)
+        return set_error(FLRL_E_NOMEM, "Cannot allocate memory");
+    const HostCfg cfg;
+    MemFl src;
+    src.rbits = bits;
+    src.rvalues = values;
+    src.direct = cfg.direct;
+    MemRawOut dst{h};
+    dst.direct = cfg.direct;
+    const int rc = fl_decompress_core(src, dst, n, F, V, std::vector<int>{dev}, cfg.workers, cfg.chunk,
+                                      "flrl_fl_decompress");
+    (void)hipSetDevice(dev);
+    if (rc) {
+        free(h);
+        return rc;
+    }
+    *out = h;
+    return FLRL_OK;
+}
+
+}  // namespace flrl
+
+using namespace flrl;
+
 extern "C" int flrl_fl_compress_file(const char *in_path, const char *out_path, int workers,
                                      size_t chunk_bytes)
 {
@@ -242,150 +797,17 @@ extern "C" int flrl_fl_compress_file(const char *in_path, const char *out_path, 
     if (!out.open(out_path))
         return set_error(FLRL_E_ARG, "[FileIO] Cannot open file: %s", out_path);
     const uint64_t F = (n + kFrame - 1) / kFrame;
-    const size_t chunk = chunk_size(chunk_bytes);
-    const size_t nchunks = n ? (size_t)((n + chunk - 1) / chunk) : 0;
-
-    Failure fail;
-    std::mutex m;
-    std::condition_variable cv;
-    fail.wait_m = &m;
-    fail.wait_cv = &cv;
-    std::vector<Ready> ready(nchunks);
-    const int nw = pipelines(W, nchunks);
-    std::vector<std::atomic<bool>> slot_free((size_t)nw * 2);
-    for (auto &f : slot_free)
-        f.store(true);
-    bool writer_stopped = false;  // under m: chunks handed over later are never read
-
-    auto worker = [&](int w) {
-        if (hipSetDevice(w % ndev) != hipSuccess) {
-            fail.set(FLRL_E_HIP, "hipSetDevice failed");
-            cv.notify_all();
-            return;
-        }
-        Slots S;
-        const size_t scr = flrl_fl_scratch_bytes(chunk);
-        if (S.alloc(chunk, chunk / kFrame, flrl_fl_values_capacity(chunk), scr) != hipSuccess) {
-            fail.set(FLRL_E_NOMEM, "Cannot allocate memory");
-            cv.notify_all();
-            return;
-        }
-        auto finish = [&](size_t c, int k) -> bool {  // stage B of chunk c in slot k
-            Slot &x = S.slot[k];
-            if (hipStreamSynchronize(x.s) != hipSuccess)
-                return false;
-            const int kerr = flrl_scratch_error(x.d_scr, x.s);
-            if (kerr) {
-                fail.set(kerr, "fl encode: device error");
-                return false;
-            }
-            const uint64_t len = (c + 1 == nchunks) ? n - (uint64_t)c * chunk : chunk;
-            const size_t fb = (size_t)((len + kFrame - 1) / kFrame);
-            const size_t vb = (size_t)x.h_u64[0];
-            if (hipMemcpyAsync(x.h_b, x.d_b, fb, hipMemcpyDeviceToHost, x.s) != hipSuccess ||
-                hipMemcpyAsync(x.h_c, x.d_c, vb, hipMemcpyDeviceToHost, x.s) != hipSuccess ||
-                hipStreamSynchronize(x.s) != hipSuccess)
-                return false;
-            std::atomic<bool> *rel = &slot_free[(size_t)w * 2 + k];
-            {
-                std::lock_guard<std::mutex> g(m);
-                if (!writer_stopped)
-                    rel->store(false);
-                Ready &r = ready[c];
-                r.bits = x.h_b;
-                r.nbits = fb;
-                r.values = x.h_c;
-                r.nvalues = vb;
-                r.released = rel;
-                r.done = true;
-            }
-            cv.notify_all();
-            return true;
-        };
-        size_t pend = SIZE_MAX;  // chunk waiting for stage B
-        int pend_k = 0;
-        int i = 0;
-        for (size_t c = (size_t)w; c < nchunks && !fail.failed.load(); c += (size_t)nw, ++i) {
-            const int k = i & 1;
-            Slot &x = S.slot[k];
-            {  // the writer must be done with this slot's previous chunk
-                std::unique_lock<std::mutex> g(m);
-                cv.wait(g, [&] { return slot_free[(size_t)w * 2 + k].load() || fail.failed.load(); });
-            }
-            if (fail.failed.load())
-                break;
-            const uint64_t off = (uint64_t)c * chunk;
-            const size_t len = (size_t)((c + 1 == nchunks) ? n - off : chunk);
-            if (debug_fail_chunk(c)) {
-                fail.set(FLRL_E_HIP, "injected failure (flrl_debug_fail_chunk)");
-                break;
-            }
-            if (!pread_all(in.fd, x.h_a, len, off)) {
-                fail.set(FLRL_E_ARG, "[FileIO] Cannot read file content");
-                break;
-            }
-            if (hipMemcpyAsync(x.d_a, x.h_a, len, hipMemcpyHostToDevice, x.s) != hipSuccess ||
-                flrl_fl_encode_device(x.d_a, len, x.d_b, x.d_c, x.d_u64, x.d_scr, x.scr_bytes, x.s) !=
-                    FLRL_OK ||
-                hipMemcpyAsync(x.h_u64, x.d_u64, 8, hipMemcpyDeviceToHost, x.s) != hipSuccess) {
-                fail.set(FLRL_E_HIP, std::string("fl encode: ") + flrl_last_error());
-                break;
-            }
-            if (pend != SIZE_MAX && !finish(pend, pend_k)) {
-                fail.set(FLRL_E_HIP, "fl encode: stream failed");
-                break;
-            }
-            pend = c;
-            pend_k = k;
-        }
-        if (!fail.failed.load() && pend != SIZE_MAX && !finish(pend, pend_k))
-            fail.set(FLRL_E_HIP, "fl encode: stream failed");
-        // keep the pinned buffers alive until the writer has released them
-        // (also after a failure: the writer may still be reading one of them)
-        std::unique_lock<std::mutex> g(m);
-        cv.wait(g, [&] { return slot_free[(size_t)w * 2].load() && slot_free[(size_t)w * 2 + 1].load(); });
-    };
-
-    std::vector<std::thread> threads;
-    for (int w = 0; w < nw && nchunks; ++w)
-        threads.emplace_back(worker, w);
-
-    // in-order writer (this thread)
-    uint64_t voff = 0;
-    for (size_t c = 0; c < nchunks; ++c) {
-        Ready r;
-        {
-            std::unique_lock<std::mutex> g(m);
-            cv.wait(g, [&] { return ready[c].done || fail.failed.load(); });
-            if (fail.failed.load())
-                break;
-            r.bits = ready[c].bits;
-            r.nbits = ready[c].nbits;
-            r.values = ready[c].values;
-            r.nvalues = ready[c].nvalues;
-            r.released = ready[c].released;
-        }
-        const uint64_t boff = kHeader + (uint64_t)c * (chunk / kFrame);
-        if (!pwrite_all(out.fd, r.bits, r.nbits, boff) ||
-            !pwrite_all(out.fd, r.values, r.nvalues, kHeader + F + voff)) {
-            fail.set(FLRL_E_ARG, "[FileIO] Cannot write to file");
-            cv.notify_all();
-            break;
-        }
-        voff += r.nvalues;
-        {
-            std::lock_guard<std::mutex> g(m);
-            r.released->store(true);
-        }
-        cv.notify_all();
-    }
-    release_unwritten(m, cv, ready, writer_stopped);
-    for (auto &t : threads)
-        t.join();
-    if (fail.failed.load())
-        return set_error(fail.code ? fail.code : FLRL_E_HIP, "%s", fail.msg.c_str());
-    const uint64_t hdr[3] = {n, F, voff};
-    if (!pwrite_all(out.fd, hdr, sizeof(hdr), 0) || !out.truncate(kHeader + F + voff) || !out.commit())
+    FdRaw src{in.fd};
+    FdFl dst{out.fd, F};
+    uint64_t V = 0;
+    const int prev = [] { int d = 0; (void)hipGetDevice(&d); return d; }();
+    const int rc = fl_compress_core(src, dst, n, all_devices(ndev), W, chunk_size(chunk_bytes), &V,
+                                    "flrl_fl_compress_file");
+    (void)hipSetDevice(prev);
+    if (rc)
+        return rc;
+    const uint64_t hdr[3] = {n, F, V};
+    if (!pwrite_all(out.fd, hdr, sizeof(hdr), 0) || !out.truncate(kHeader + F + V) || !out.commit())
         return set_error(FLRL_E_ARG, "[FileIO] Cannot write to file");
     return FLRL_OK;
 }
@@ -426,122 +848,16 @@ extern "C" int flrl_fl_decompress_file(const char *in_path, const char *out_path
             return set_error(FLRL_E_ARG, "[FileIO] Cannot write to file");
         return FLRL_OK;
     }
-    const size_t chunk = chunk_size(chunk_bytes);
-    const size_t cf = chunk / kFrame;  // frames per chunk
-    const size_t nchunks = (size_t)((n + chunk - 1) / chunk);
-    // value offset of every chunk = 16 x (widths of all earlier frames): one
-    // streamed pass over the widths (host memory bounded by a 4 MiB window, not
-    // F = n/128 bytes); the workers then read each chunk's widths themselves
-    std::vector<uint64_t> voff(nchunks + 1);
-    {
-        std::vector<uint8_t> win(4u << 20);
-        uint64_t acc = 0, cur = 0;  // cur: width sum of the current chunk so far
-        for (uint64_t f0 = 0; f0 < F;) {
-            const size_t k = (size_t)(F - f0 < win.size() ? F - f0 : win.size());
-            if (!pread_all(in.fd, win.data(), k, kHeader + f0))
-                return set_error(FLRL_E_ARG, "[FileIO] Cannot read file content");
-            for (size_t i = 0; i < k; ++i) {
-                const uint64_t f = f0 + i;
-                if (f % cf == 0) {
-                    acc += 16 * cur;
-                    voff[(size_t)(f / cf)] = acc;
-                    cur = 0;
-                }
-                const uint8_t b = win[i];
-                if (b < 1 || b > 8)
-                    return set_error(FLRL_E_FORMAT, "invalid frame width %u at frame %llu", b,
-                                     (unsigned long long)f);
-                cur += b;
-            }
-            f0 += k;
-        }
-        voff[nchunks] = V;
-        if (voff[nchunks - 1] > V)
-            return set_error(FLRL_E_FORMAT, "valuesSize %llu smaller than the widths imply",
-                             (unsigned long long)V);
-    }
     if (!out.truncate(n))
         return set_error(FLRL_E_ARG, "[FileIO] Cannot write to file");
-
-    Failure fail;
-    const int nw = pipelines(W, nchunks);
-    auto worker = [&](int w) {
-        if (hipSetDevice(w % ndev) != hipSuccess) {
-            fail.set(FLRL_E_HIP, "hipSetDevice failed");
-            return;
-        }
-        Slots S;
-        const size_t vcap = flrl_fl_values_capacity(chunk);
-        if (S.alloc(cf, vcap, chunk, flrl_fl_scratch_bytes(chunk)) != hipSuccess) {
-            fail.set(FLRL_E_NOMEM, "Cannot allocate memory");
-            return;
-        }
-        auto finish = [&](size_t c, int k) -> bool {  // wait, check, write chunk c
-            Slot &x = S.slot[k];
-            if (hipStreamSynchronize(x.s) != hipSuccess) {
-                fail.set(FLRL_E_HIP, "fl decode: stream failed");
-                return false;
-            }
-            const int kerr = flrl_scratch_error(x.d_scr, x.s);
-            if (kerr) {
-                fail.set(kerr, "fl decode: malformed data (widths or valuesSize)");
-                return false;
-            }
-            const uint64_t off = (uint64_t)c * chunk;
-            const size_t len = (size_t)((c + 1 == nchunks) ? n - off : chunk);
-            if (!pwrite_all(out.fd, x.h_c, len, off)) {
-                fail.set(FLRL_E_ARG, "[FileIO] Cannot write to file");
-                return false;
-            }
-            return true;
-        };
-        size_t pend = SIZE_MAX;
-        int pend_k = 0;
-        int i = 0;
-        for (size_t c = (size_t)w; c < nchunks && !fail.failed.load(); c += (size_t)nw, ++i) {
-            const int k = i & 1;
-            Slot &x = S.slot[k];
-            // slot k last held chunk c - 2*nw, finished (written) in the previous iteration
-            const uint64_t off = (uint64_t)c * chunk;
-            const size_t len = (size_t)((c + 1 == nchunks) ? n - off : chunk);
-            const size_t fb = (len + kFrame - 1) / kFrame;
-            const uint64_t vo = voff[c], vb = voff[c + 1] - voff[c];
-            if (vb > vcap) {
-                fail.set(FLRL_E_FORMAT, "valuesSize larger than the widths imply");
-                break;
-            }
-            if (debug_fail_chunk(c)) {
-                fail.set(FLRL_E_HIP, "injected failure (flrl_debug_fail_chunk)");
-                break;
-            }
-            if (!pread_all(in.fd, x.h_a, fb, kHeader + (uint64_t)c * cf) ||
-                !pread_all(in.fd, x.h_b, (size_t)vb, kHeader + F + vo)) {
-                fail.set(FLRL_E_ARG, "[FileIO] Cannot read file content");
-                break;
-            }
-            if (hipMemcpyAsync(x.d_a, x.h_a, fb, hipMemcpyHostToDevice, x.s) != hipSuccess ||
-                hipMemcpyAsync(x.d_b, x.h_b, (size_t)vb, hipMemcpyHostToDevice, x.s) != hipSuccess ||
-                flrl_fl_decode_device(x.d_a, fb, x.d_b, (size_t)vb, x.d_c, len, x.d_scr, x.scr_bytes, x.s) !=
-                    FLRL_OK ||
-                hipMemcpyAsync(x.h_c, x.d_c, len, hipMemcpyDeviceToHost, x.s) != hipSuccess) {
-                fail.set(FLRL_E_HIP, std::string("fl decode: ") + flrl_last_error());
-                break;
-            }
-            if (pend != SIZE_MAX && !finish(pend, pend_k))
-                break;
-            pend = c;
-            pend_k = k;
-        }
-        if (!fail.failed.load() && pend != SIZE_MAX)
-            (void)finish(pend, pend_k);
-    };
-    std::vector<std::thread> threads;
-    for (int w = 0; w < nw; ++w)
-        threads.emplace_back(worker, w);
-    for (auto &t : threads)
-        t.join();
-    if (fail.failed.load())
-        return set_error(fail.code ? fail.code : FLRL_E_HIP, "%s", fail.msg.c_str());
+    FdFl src{in.fd, F};
+    FdRaw dst{out.fd};
+    const int prev = [] { int d = 0; (void)hipGetDevice(&d); return d; }();
+    const int rc = fl_decompress_core(src, dst, n, F, V, all_devices(ndev), W, chunk_size(chunk_bytes),
+                                      "flrl_fl_decompress_file");
+    (void)hipSetDevice(prev);
+    if (rc)
+        return rc;
     if (!out.commit())
         return set_error(FLRL_E_ARG, "[FileIO] Cannot write to file");
     return FLRL_OK;

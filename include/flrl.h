@@ -68,7 +68,10 @@ int flrl_device_count(void);             /* number of visible HIP devices (0 if 
 /* ---- FL, host buffers (synchronous) ---------------------------------------
  * flrl_fl_compress replaces FixedLength::gpuCompress (src/fl/fl_gpu.cuh:14,
  * fl_gpu.cu:289-423) and its CPU twin cpuCompress (src/fl/fl_cpu.cuh:9). On
- * size == 0 it returns an all-zero flrl_fl_buf (fl_gpu.cu:291-294). */
+ * size == 0 it returns an all-zero flrl_fl_buf (fl_gpu.cu:291-294). Runs on
+ * the current device through pinned staging in 16 MiB chunks, 4 pipelines with
+ * two chunks in flight each (the staging is allocated once and kept for
+ * later calls), so host copies, PCIe transfers and the kernels overlap. */
 int flrl_fl_compress(const uint8_t *data, size_t size, flrl_fl_buf *out);
 
 /* Replaces FixedLength::gpuDecompress (src/fl/fl_gpu.cuh:15, fl_gpu.cu:537-645)
@@ -163,7 +166,9 @@ int flrl_fl_encode_sharded(flrl_comm *c, int nshards, const uint8_t *const *d_in
  * flrl_fl_compress + the FL container (file_io.cu:222-280). Decompression
  * validates the header (bitsSize == ceil(inputSize/128), file length ==
  * 24 + bitsSize + valuesSize) and every width before decoding (FLRL_E_FORMAT).
- * On error the output file may be partial; the caller removes it. */
+ * Outputs go to a temporary file next to out_path, renamed into place on
+ * success: on error an existing output is left as it was, and in_path may
+ * equal out_path. */
 int flrl_fl_compress_file(const char *in_path, const char *out_path, int workers, size_t chunk_bytes);
 int flrl_fl_decompress_file(const char *in_path, const char *out_path, int workers, size_t chunk_bytes);
 

@@ -5,9 +5,12 @@ Compares, on one synthetic input file (u8 for FL, runs32 for RL):
   whole   read file -> flrl_fl_compress (host buffers: H2D, encode, D2H,
           synchronous, the reference gpuCompress shape) -> write .fl
   stream  flrl_fl_compress_file (chunked, pipelined; workers = 1 and = GPUs)
-and the same for decompression. Prints one JSON line. Not part of bench.py's
-metric (that one is device-resident).
-Usage: bench_stream.py [--bytes N] [--kind u8] [--dir DIR] [--reps R]
+and the same for decompression, plus the host-buffer C API memory to memory
+(flrl_fl_compress / flrl_fl_decompress through their pinned chunk pipelines,
+timed around the raw C calls) next to the PCIe copy ceiling (torch copies of
+the same bytes between pinned host memory and HBM). Prints one JSON line. Not
+part of bench.py's metric (that one is device-resident).
+Usage: bench_stream.py [--bytes N] [--kind u8] [--dir DIR] [--reps R] [--mem-only]
 """
 import argparse
 import json
@@ -31,13 +34,97 @@ def best(fn, reps):
     return min(ts)
 
 
+def mem_rates(n: int, kind: str, reps: int, ceiling: bool = True) -> dict:
+    """flrl_fl_compress / flrl_fl_decompress memory to memory vs the PCIe ceiling."""
+    import ctypes
+
+    import numpy as np
+    import torch
+    kinds = {"u8": 0, "lo4": 1, "zero": 2}
+    x = flrl.gen_host(kinds[kind], n, 42)
+    lib = flrl._lib
+    res = {"bytes": n, "kind": kind, "api": "flrl_fl_compress / flrl_fl_decompress (host buffers)"}
+
+    def comp():
+        b = flrl._FLBuf()
+        flrl._check(lib.flrl_fl_compress(x.ctypes.data, n, ctypes.byref(b)))
+        return b
+
+    b = comp()
+    bits = np.ctypeslib.as_array(ctypes.cast(b.bits, ctypes.POINTER(ctypes.c_uint8)), (b.bits_size,)).copy()
+    vals = np.ctypeslib.as_array(ctypes.cast(b.values, ctypes.POINTER(ctypes.c_uint8)), (b.values_size,)).copy()
+    flrl._libc.free(ctypes.cast(b.bits, ctypes.c_void_p).value)
+    flrl._libc.free(ctypes.cast(b.values, ctypes.c_void_p).value)
+
+    def comp_free():
+        b = comp()
+        flrl._libc.free(ctypes.cast(b.bits, ctypes.c_void_p).value)
+        flrl._libc.free(ctypes.cast(b.values, ctypes.c_void_p).value)
+
+    def decomp():
+        o, on = flrl._u8p(), ctypes.c_size_t(0)
+        flrl._check(lib.flrl_fl_decompress(n, bits.ctypes.data, bits.size, vals.ctypes.data, vals.size,
+                                           ctypes.byref(o), ctypes.byref(on)))
+        return o
+
+    o = decomp()
+    back = np.ctypeslib.as_array(ctypes.cast(o, ctypes.POINTER(ctypes.c_uint8)), (n,))
+    res["roundtrip_ok"] = bool(np.array_equal(back, x))
+    flrl._libc.free(ctypes.cast(o, ctypes.c_void_p).value)
+
+    def decomp_free():
+        flrl._libc.free(ctypes.cast(decomp(), ctypes.c_void_p).value)
+
+    tc, td = best(comp_free, reps), best(decomp_free, reps)
+    res["compress_GBps"] = n / tc / 1e9
+    res["decompress_GBps"] = n / td / 1e9
+    res["compress_moved_GBps"] = (n + bits.size + vals.size) / tc / 1e9
+    res["decompress_moved_GBps"] = (n + bits.size + vals.size) / td / 1e9
+    def first_touch():
+        y = np.empty(n, dtype=np.uint8)  # fresh pages: what a malloc'd output costs
+        y.fill(1)
+    res["host_first_touch_GBps"] = n / best(first_touch, reps) / 1e9
+    if not ceiling:
+        return {k: (round(v, 3) if isinstance(v, float) else v) for k, v in res.items()}
+    # PCIe ceiling: one torch copy each way of n bytes, pinned and pageable host memory
+    h = torch.empty(n, dtype=torch.uint8, pin_memory=True)
+    g = torch.empty(n, dtype=torch.uint8, device="cuda")
+    p = torch.from_numpy(x)
+
+    def cp(dst, src):
+        def f():
+            dst.copy_(src, non_blocking=True)
+            torch.cuda.synchronize()
+        return f
+    res["pcie_h2d_pinned_GBps"] = n / best(cp(g, h), reps) / 1e9
+    res["pcie_d2h_pinned_GBps"] = n / best(cp(h, g), reps) / 1e9
+    res["pcie_h2d_pageable_GBps"] = n / best(cp(g, p), reps) / 1e9
+    res["host_memcpy_1thread_GBps"] = n / best(lambda: h.copy_(p), reps) / 1e9
+    return {k: (round(v, 3) if isinstance(v, float) else v) for k, v in res.items()}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--bytes", type=int, default=1 << 30)
     ap.add_argument("--kind", default="u8")
     ap.add_argument("--dir", default=None)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--mem-only", action="store_true")
+    ap.add_argument("--sweep", action="store_true",
+                    help="with --mem-only: host API rates over FLRL_HOST_{DIRECT,WORKERS,CHUNK}")
     a = ap.parse_args()
+    if a.mem_only and a.sweep:
+        for thp in ("0", "1"):
+            for direct in ("0", "1"):
+                for w, ch in (("4", str(16 << 20)), ("8", str(16 << 20)), ("8", str(32 << 20))):
+                    os.environ.update(FLRL_HOST_DIRECT=direct, FLRL_HOST_WORKERS=w, FLRL_HOST_CHUNK=ch,
+                                      FLRL_HOST_THP=thp)
+                    r = mem_rates(a.bytes, a.kind, a.reps, ceiling=False)
+                    print(json.dumps({"thp": thp, "direct": direct, "workers": w, "chunk": ch, **r}), flush=True)
+        return
+    if a.mem_only:
+        print(json.dumps(mem_rates(a.bytes, a.kind, a.reps)))
+        return
     kinds = {"u8": 0, "lo4": 1, "zero": 2}
     d = tempfile.mkdtemp(dir=a.dir)
     src, dst, back = (os.path.join(d, x) for x in ("in", "out.fl", "back"))
