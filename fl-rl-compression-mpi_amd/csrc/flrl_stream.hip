@@ -670,9 +670,13 @@ std::vector<int> all_devices(int ndev)
 }  // namespace
 
 // Host-buffer FL (flrl_fl_compress / flrl_fl_decompress, flrl_fl.hip): the
-// same pipelines memory to memory on the current device, kHostWorkers wide
-// (host memcpy into pinned staging is the per-pipeline limit, not PCIe).
-constexpr int kHostWorkers = 4;
+// same pipelines memory to memory on the current device, kHostWorkers wide.
+// Measured on 2 GiB u8 (scripts/bench_stream.py --mem-only --sweep, DESIGN.md
+// §4): the first touch of the freshly malloc'd output pages bounds the call
+// (~10 GB/s single-threaded), not PCIe (57 GB/s each way); huge pages for the
+// outputs roughly double the rate; 8 pipelines x 16 MiB chunks through pinned
+// staging beat direct hipMemcpyAsync from/to the pageable buffers.
+constexpr int kHostWorkers = 8;
 constexpr size_t kHostChunk = 16ull << 20;
 struct HostCfg {
     int workers = kHostWorkers;
@@ -695,7 +699,8 @@ struct HostCfg {
 uint8_t *host_alloc(size_t bytes)
 {
     uint8_t *p = static_cast<uint8_t *>(malloc(bytes ? bytes : 1));
-    if (p && bytes >= (8u << 20) && getenv("FLRL_HOST_THP") && atoi(getenv("FLRL_HOST_THP"))) {
+    const char *thp = getenv("FLRL_HOST_THP");  // "0": plain pages (A/B)
+    if (p && bytes >= (8u << 20) && !(thp && atoi(thp) == 0)) {
         const uintptr_t a = ((uintptr_t)p + (2u << 20) - 1) & ~(uintptr_t)((2u << 20) - 1);
         const uintptr_t e = ((uintptr_t)p + bytes) & ~(uintptr_t)((2u << 20) - 1);
         if (e > a)

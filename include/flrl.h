@@ -69,7 +69,7 @@ int flrl_device_count(void);             /* number of visible HIP devices (0 if 
  * flrl_fl_compress replaces FixedLength::gpuCompress (src/fl/fl_gpu.cuh:14,
  * fl_gpu.cu:289-423) and its CPU twin cpuCompress (src/fl/fl_cpu.cuh:9). On
  * size == 0 it returns an all-zero flrl_fl_buf (fl_gpu.cu:291-294). Runs on
- * the current device through pinned staging in 16 MiB chunks, 4 pipelines with
+ * the current device through pinned staging in 16 MiB chunks, 8 pipelines with
  * two chunks in flight each (the staging is allocated once and kept for
  * later calls), so host copies, PCIe transfers and the kernels overlap. */
 int flrl_fl_compress(const uint8_t *data, size_t size, flrl_fl_buf *out);
