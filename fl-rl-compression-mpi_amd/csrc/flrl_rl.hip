@@ -48,13 +48,18 @@
 #ifndef FLRL_RL_ABL
 #define FLRL_RL_ABL 0
 #endif
+// Per-tile timestamps (scripts/ubench_rl.hip -DTRACE): 0 ticket, 1 all waves
+// scanned, 2 map published, 3 look-back resolved, 4 wave 0 emitted.
+#ifndef FLRL_RL_TRACE
+#define FLRL_RL_TRACE(tile, k) ((void)0)
+#endif
 
 namespace flrl {
 
 #ifndef FLRL_RL_LB
 #define FLRL_RL_LB 64
 #endif
-constexpr int kRlThreads = 256;                     // encode workgroup: 4 waves (LB 64: 94 VGPRs, 32 KiB LDS, 5 per CU)
+constexpr int kRlThreads = 256;                     // encode workgroup: 4 waves (LB 64: 94 VGPRs, < 32 KiB LDS, 5 per CU)
 constexpr int kRlLaneBytes = FLRL_RL_LB;            // contiguous bytes per lane (64 or 128)
 constexpr int kRlSub = 32768 / (64 * kRlLaneBytes); // sub-chunks per wave chunk (one look-back per tile)
 constexpr int kRlTileBytes = kRlLaneBytes * kRlThreads * kRlSub;  // 128 KiB: 4 waves x 32 KiB
@@ -62,7 +67,10 @@ constexpr int kRlTileBytes = kRlLaneBytes * kRlThreads * kRlSub;  // 128 KiB: 4 
 #define FLRL_RL_LOOKG 1
 #endif
 constexpr int kRlLookG = FLRL_RL_LOOKG;  // look-back granules per lane (window 64 G tiles)
-constexpr int kRlStageBytes = 16256;  // LDS run staging (48 KiB of LDS per workgroup)
+#ifndef FLRL_RL_STAGE
+#define FLRL_RL_STAGE 15360
+#endif
+constexpr int kRlStageBytes = FLRL_RL_STAGE;  // LDS run staging per workgroup
 
 constexpr int kRdRuns = 4096;        // runs per decode tile
 constexpr int kRdThreads = 256;
@@ -352,6 +360,7 @@ __global__ __launch_bounds__(T) void rl_encode_wave_kernel(
             raise_error(ctrl, FLRL_E_ARG);
         return;
     }
+    FLRL_RL_TRACE(tile, 0);
     const uint64_t chunk_off = (uint64_t)tile * TBT + (uint64_t)w * CB;
     const uint32_t chunk_len = chunk_off >= n ? 0u : (n - chunk_off < (uint64_t)CB ? (uint32_t)(n - chunk_off) : (uint32_t)CB);
     const int ns = (int)((chunk_len + WB - 1) / WB);  // sub-chunks of this wave
@@ -561,6 +570,7 @@ __global__ __launch_bounds__(T) void rl_encode_wave_kernel(
     if (lane == 0)
         s_map[w] = first != kNone ? sm_nat(first, K, rel_in & 0xFFu) : sm_nonat(chunk_len);
     __syncthreads();
+    FLRL_RL_TRACE(tile, 1);
     if (w == 0) {
         uint64_t tmap = s_map[0];
 #pragma unroll
@@ -571,7 +581,9 @@ __global__ __launch_bounds__(T) void rl_encode_wave_kernel(
             st = sm_const((uint64_t)tile * 4096u, 0);
         } else {
             publish_seg(status, tile, tmap);
+            FLRL_RL_TRACE(tile, 2);
             st = lookback_seg<kRlLookG>(status, tile, tmap, ctrl);
+            FLRL_RL_TRACE(tile, 3);
         }
         if (lane == 0) {
 #pragma unroll
@@ -692,6 +704,7 @@ __global__ __launch_bounds__(T) void rl_encode_wave_kernel(
         }
     }
 
+    FLRL_RL_TRACE(tile, 4);
     // ---- the final run (ends at byte n-1): the wave whose chunk holds it ----
     if (chunk_off + chunk_len == n && lane == 0) {
         const uint64_t R = h_in + splits(c_in, pre) + K;

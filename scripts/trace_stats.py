@@ -1,14 +1,14 @@
-"""Summarise a per-tile timestamp trace written by scripts/ubench_{fl,rl}.bin -DTRACE:
-u64[tiles][4] s_memrealtime (100 MHz) at tile start / aggregate published /
-look-back resolved / stores issued."""
+"""Summarise a per-tile timestamp trace written by scripts/ubench_rl.bin -DTRACE:
+u64[tiles][8] s_memrealtime (100 MHz): 0 ticket, 1 all waves scanned, 2 map
+published, 3 look-back resolved, 4 wave 0 emitted (flrl_rl.hip FLRL_RL_TRACE)."""
 import sys
 
 import numpy as np
 
-t = np.fromfile(sys.argv[1], dtype=np.uint64).reshape(-1, 4).astype(np.int64)
+t = np.fromfile(sys.argv[1], dtype=np.uint64).reshape(-1, 8)[:, :5].astype(np.int64)
 t0 = t[t > 0].min()
 t = (t - t0) * 10 / 1000.0  # us
-start, pub, lb, end = t[:, 0], t[:, 1], t[:, 2], t[:, 3]
+start, scanned, pub, lb, end = t[:, 0], t[:, 1], t[:, 2], t[:, 3], t[:, 4]
 print(f"tiles {len(t)}  span {end.max() - start.min():.1f} us")
 
 
@@ -17,12 +17,19 @@ def pct(x, name):
           f"p90 {np.percentile(x, 90):7.2f}  mean {x.mean():7.2f}")
 
 
-pct(pub - start, "start -> aggregate published")
+pct(scanned - start, "start -> all waves scanned")
+pct(pub - scanned, "scanned -> map published")
 pct(lb - pub, "published -> look-back resolved")
 pct(end - lb, "resolved -> stores issued")
 pct(pub[1:] - pub[:-1], "pub[t] - pub[t-1]")
 print("fraction of tiles whose predecessor published later:", round(float((pub[:-1] > pub[1:]).mean()), 3))
 pct(lb[1:] - lb[:-1], "lb[t] - lb[t-1]")
 i = len(t) // 2
+busy = np.zeros(int(end.max()) + 2)
+for a, b in zip(start, end):  # tiles in flight per us
+    busy[int(a):int(b) + 1] += 1
+print("tiles in flight: mean", round(float(busy[busy > 0].mean()), 1), "max", int(busy.max()))
+w = lb - pub
+print("look-back wait share of tile time:", round(float(w.sum() / (end - start).sum()), 3))
 for k in range(i, i + 10):
     print(k, *(round(float(v), 2) for v in t[k]))
