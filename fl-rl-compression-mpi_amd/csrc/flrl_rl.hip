@@ -53,13 +53,26 @@
 #ifndef FLRL_RL_TRACE
 #define FLRL_RL_TRACE(tile, k) ((void)0)
 #endif
+// Priority of wave 0 while it publishes and looks back (s_setprio; 0: none):
+// it shares its SIMD with the staging passes of up to four other waves.
+#ifndef FLRL_RL_LB_PRIO
+#define FLRL_RL_LB_PRIO 0
+#endif
+// Look-back statistics of one call (trace builds): polls that found an
+// unpublished predecessor, and windows composed.
+#ifndef FLRL_RL_LB_STAT
+#define FLRL_RL_LB_STAT(tile, spins, rounds) ((void)(spins), (void)(rounds))
+#endif
 
 namespace flrl {
 
 #ifndef FLRL_RL_LB
 #define FLRL_RL_LB 64
 #endif
-constexpr int kRlThreads = 256;                     // encode workgroup: 4 waves (LB 64: 94 VGPRs, < 32 KiB LDS, 5 per CU)
+#ifndef FLRL_RL_THREADS
+#define FLRL_RL_THREADS 256
+#endif
+constexpr int kRlThreads = FLRL_RL_THREADS;         // encode workgroup: 4 waves (LB 64: 94 VGPRs, < 32 KiB LDS, 5 per CU)
 constexpr int kRlLaneBytes = FLRL_RL_LB;            // contiguous bytes per lane (64 or 128)
 constexpr int kRlSub = 32768 / (64 * kRlLaneBytes); // sub-chunks per wave chunk (one look-back per tile)
 constexpr int kRlTileBytes = kRlLaneBytes * kRlThreads * kRlSub;  // 128 KiB: 4 waves x 32 KiB
@@ -204,6 +217,21 @@ __device__ __forceinline__ void publish_seg(uint64_t *status, uint32_t tile, uin
                                                : (kFlagA | map));
 }
 
+// DPP move of a u64 from a higher lane (row_shl:k within 16-lane rows; lanes
+// without a source read 0) and a wave-uniform read of a lane's u64.
+template <int CTRL>
+__device__ __forceinline__ uint64_t dpp_dn64(uint64_t v)
+{
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)v, CTRL, 0xF, 0xF, true);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(v >> 32), CTRL, 0xF, 0xF, true);
+    return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, int l)
+{
+    return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l) << 32) |
+           (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+}
+
 template <int G>
 __device__ __forceinline__ uint64_t lookback_seg(uint64_t *status, uint32_t tile, uint64_t map,
                                                  Ctrl *ctrl)
@@ -217,8 +245,9 @@ __device__ __forceinline__ uint64_t lookback_seg(uint64_t *status, uint32_t tile
     uint64_t acc_a = 0, acc_b = 0;
     uint32_t acc_c = 0;
     int64_t j = (int64_t)tile - 1;
-    uint32_t spins = 0;
+    uint32_t spins = 0, rounds = 0;
     for (;;) {
+        ++rounds;
         const int64_t idx = j - (int64_t)lane * G;
         uint64_t s[G];
         uint64_t m;
@@ -261,14 +290,16 @@ __device__ __forceinline__ uint64_t lookback_seg(uint64_t *status, uint32_t tile
         const int first = pm ? __ffsll(pm) - 1 : kWave;
         if (lane > first)
             m = sm_nonat(0);
-        // suffix composition: lane l ends with compose(m_63 .. m_l); identity = no-nat L 0
-#pragma unroll
-        for (int o = 1; o < kWave; o <<= 1) {
-            const uint64_t older = __shfl_down(m, o, kWave);
-            if (lane + o < kWave)
-                m = sm_compose(older, m);
-        }
-        const uint64_t win = __shfl(m, 0, kWave);  // oldest-first composition of the window
+        // composition of the window, oldest first (identity: no-nat L 0 = 0):
+        // four DPP row_shl steps compose each 16-lane row into its lane 0 (lanes
+        // past a row read 0), then the four row results are composed
+        m = sm_compose(dpp_dn64<0x101>(m), m);
+        m = sm_compose(dpp_dn64<0x102>(m), m);
+        m = sm_compose(dpp_dn64<0x104>(m), m);
+        m = sm_compose(dpp_dn64<0x108>(m), m);
+        const uint64_t win = sm_compose(sm_compose(sm_compose(readlane64(m, 48), readlane64(m, 32)),
+                                                   readlane64(m, 16)),
+                                        readlane64(m, 0));
         // combine with the newer accumulator: win then acc
         uint64_t res;
         if ((win & kSmKind) == kSmConst) {
@@ -284,6 +315,7 @@ __device__ __forceinline__ uint64_t lookback_seg(uint64_t *status, uint32_t tile
             res = sm_const(H, c);
             if (lane == 0)
                 granule_store(&status[tile], kFlagP | sm_compose(res, map));
+            FLRL_RL_LB_STAT(tile, spins, rounds);
             return res;
         }
         // no inclusive prefix in this window: fold it into the accumulator
@@ -304,76 +336,89 @@ __device__ __forceinline__ uint64_t lookback_seg(uint64_t *status, uint32_t tile
     }
 }
 
-// RL encode. A tile is 128 KiB taken by ticket; wave w owns its w-th
+// RL encode, per wave. A tile is 128 KiB; wave w of its workgroup owns the w-th
 // contiguous 32 KiB chunk and streams it as SUB sub-chunks of 64*LB bytes
 // through its OWN slice of LDS (registers -> ds_write -> each lane reads its LB
 // contiguous bytes; LDS ops of one wave are in order, so no barrier), with the
 // next sub-chunk's loads in flight during each scan. The image is swizzled so
 // that those lane reads are bank-conflict free: row r keeps its 16-byte chunk c
 // at r*LB + ((c ^ swz(r)) * 16). LB < 255, so a lane holds at most one split
-// head, before its first natural head. All scans are wave scans with
-// the carries (PhaseMap, first natural head, state-independent head count) in
-// uniform registers, and each wave stages its own state-independent runs, so a
-// tile has three block barriers (ticket, wave maps, state) instead of four per
-// sub-tile. The wave maps compose (sm_compose) into the tile's map for the one
-// look-back; the resolved state is then advanced wave by wave, and every wave
-// emits its own prefix (split heads before its first natural head), staged runs
-// and, past a staging overflow, re-read sub-chunks: sparse ones through the
-// staging area, dense ones one lane row at a time (contiguous stores).
-template <int T, int LB, int SUB>
-__global__ __launch_bounds__(T) void rl_encode_wave_kernel(
-    const uint8_t *__restrict__ in, uint64_t n, uint32_t ntiles, uint8_t *__restrict__ counts,
-    uint8_t *__restrict__ values, uint64_t *__restrict__ runs_out, Ctrl *ctrl, uint64_t *status)
-{
-    constexpr int W = T / kWave;
-    constexpr int CH = LB / 16;      // 16-byte chunks per lane
-    constexpr int WB = kWave * LB;   // sub-chunk bytes
-    constexpr int CB = WB * SUB;     // wave chunk bytes
-    constexpr int TBT = CB * W;      // tile bytes
-    constexpr int SW = kRlStageBytes / W / 2;  // staged records per wave
-    constexpr int NJ = WB / 1024;    // 1 KiB wave-loads per sub-chunk
-    constexpr uint32_t kNone = 0xFFFFFFFFu;
+// head, before its first natural head. All scans are wave scans with the
+// carries (PhaseMap, first natural head, state-independent head count) in
+// uniform registers, and each wave stages its own state-independent runs. The
+// wave maps compose (sm_compose) into the tile's map for the one look-back; the
+// resolved state is then advanced wave by wave, and every wave emits its own
+// prefix (split heads before its first natural head), staged runs and, past a
+// staging overflow, re-read sub-chunks: sparse ones through the staging area,
+// dense ones one lane row at a time (contiguous stores).
+template <int LB, int SUB, int W>
+struct RlWave {
+    static constexpr int CH = LB / 16;      // 16-byte chunks per lane
+    static constexpr int WB = kWave * LB;   // sub-chunk bytes
+    static constexpr int CB = WB * SUB;     // wave chunk bytes
+    static constexpr int TBT = CB * W;      // tile bytes
+    static constexpr int SW = kRlStageBytes / W / 2;  // staged records per wave
+    static constexpr int NJ = WB / 1024;    // 1 KiB wave-loads per sub-chunk
+    static constexpr int RPL = 1024 / LB;   // image rows per wave-load
+    static constexpr uint32_t kNone = 0xFFFFFFFFu;
     static_assert(LB == 128 || LB == 64, "one or two u64 head masks per lane");
     static_assert(TBT == kRlTileBytes, "tile geometry shared with the layout");
-    __shared__ __attribute__((aligned(16))) uint8_t s_lds[W * WB + kRlStageBytes];
-    __shared__ uint64_t s_map[W];
-    __shared__ uint64_t s_st[W];
-    __shared__ uint32_t s_ticket;
 
-    const int tid = threadIdx.x;
-    const int lane = tid & (kWave - 1);
-    const int w = tid / kWave;
-    uint8_t *const img = s_lds + w * WB;
-    uint8_t *const stc = s_lds + W * WB + w * 2 * SW;
-    uint8_t *const stv = stc + SW;
-    const uint32_t row = (uint32_t)lane;
-    const uint32_t o = row * LB;
-    const uint8_t *my = img + o;
+    struct Sub {
+        uint32_t nat[CH / 2];  // 16-bit natural-head masks, two per word
+        uint32_t ncnt, fpos, lpos, vbl, p0;
+        uint32_t lrel;    // lane start state from the sub-chunk's start (PhaseMap)
+        uint32_t smap;    // the sub-chunk's PhaseMap
+        uint32_t sfirst;  // first natural head in the sub-chunk (kNone: none)
+    };
+    // A wave chunk after the staging pass (wave-uniform values).
+    struct Chunk {
+        uint64_t off;     // first byte
+        uint32_t len;     // bytes (0: past the input)
+        int ns;           // sub-chunks
+        int nst;          // sub-chunks whose runs are all staged
+        uint32_t first;   // first natural head (chunk-relative; kNone: none)
+        uint32_t K;       // state-independent heads (runs ended by the heads from `first` on)
+        uint32_t Kst;     // of them staged
+        uint32_t rel_in;  // PhaseMap over the whole chunk
+        uint32_t rel_st;  // PhaseMap over the staged sub-chunks
+        uint32_t v0;      // the chunk's first byte
+        __device__ uint32_t pre() const { return first != kNone ? first : len; }
+        __device__ uint64_t map() const { return first != kNone ? sm_nat(first, K, rel_in & 0xFFu) : sm_nonat(len); }
+    };
+
+    const uint8_t *in;
+    uint64_t n;
+    uint8_t *img, *stc, *stv;
+    const uint8_t *my;
+    int lane;
+    uint32_t row, o, sw, swz_c;
+
     // swizzle of row r: its chunk c sits at position c ^ swz(r); 16 lanes of a
     // ds_read_b128 (rows r..r+15, one chunk each) then cover all 64 banks
-    auto swz = [](uint32_t r) -> uint32_t { return LB == 128 ? (r & 7u) : ((r >> 2) & 3u); };
-    const uint32_t sw = swz(row);
+    __device__ static uint32_t swz(uint32_t r) { return LB == 128 ? (r & 7u) : ((r >> 2) & 3u); }
 
-    const uint32_t tile = take_ticket(ctrl, &s_ticket);
-    if (tile >= ntiles) {  // the scratch's ticket was not reset for this launch
-        if (threadIdx.x == 0)
-            raise_error(ctrl, FLRL_E_ARG);
-        return;
+    __device__ RlWave(const uint8_t *in_, uint64_t n_, uint8_t *lds, int w) : in(in_), n(n_)
+    {
+        lane = threadIdx.x & (kWave - 1);
+        img = lds + w * WB;
+        stc = lds + W * WB + w * 2 * SW;
+        stv = stc + SW;
+        row = (uint32_t)lane;
+        o = row * LB;
+        my = img + o;
+        sw = swz(row);
+        // LDS slot (j, lane) = byte j*1024 + lane*16 = row j*RPL + lane/CH, position
+        // lane % CH; swz(row) depends on lane/CH only, as RPL is a multiple of 8
+        // (LB 128) or 16 (LB 64)
+        swz_c = ((uint32_t)lane % CH) ^ swz((uint32_t)lane / CH);
     }
-    FLRL_RL_TRACE(tile, 0);
-    const uint64_t chunk_off = (uint64_t)tile * TBT + (uint64_t)w * CB;
-    const uint32_t chunk_len = chunk_off >= n ? 0u : (n - chunk_off < (uint64_t)CB ? (uint32_t)(n - chunk_off) : (uint32_t)CB);
-    const int ns = (int)((chunk_len + WB - 1) / WB);  // sub-chunks of this wave
-    // LDS slot (j, lane) = byte j*1024 + lane*16 = row j*RPL + lane/CH, position
-    // lane % CH; swz(row) depends on lane/CH only, as RPL is a multiple of 8 (LB
-    // 128) or 16 (LB 64)
-    constexpr int RPL = 1024 / LB;  // rows per wave-load
-    const uint32_t swz_c = ((uint32_t)lane % CH) ^ swz((uint32_t)lane / CH);
 
-    // sub-chunk s into registers, placed as the LDS image wants it, each
-    // wave-load 1 KiB of LDS
-    auto load_sub = [&](int s, u32x4 (&pf)[NJ]) {
-        const uint64_t so = chunk_off + (uint64_t)s * WB;
+    // sub-chunk s of the chunk at `off` into registers, placed as the LDS image
+    // wants it, each wave-load 1 KiB of LDS
+    __device__ void load_sub(uint64_t off, int s, u32x4 (&pf)[NJ]) const
+    {
+        const uint64_t so = off + (uint64_t)s * WB;
         if (so + WB <= n) {
 #pragma unroll
             for (int j = 0; j < NJ; ++j)
@@ -384,24 +429,19 @@ __global__ __launch_bounds__(T) void rl_encode_wave_kernel(
             for (int j = 0; j < NJ; ++j)
                 pf[j] = load16_tail(in, so + (uint32_t)(j * RPL + lane / CH) * LB + swz_c * 16, n);
         }
-    };
-    struct Sub {
-        uint32_t nat[CH / 2];  // 16-bit masks, two per word (CH >= 4)
-        uint32_t ncnt, fpos, lpos, vbl, p0;
-        uint32_t lrel;    // lane start state from the sub-chunk's start (PhaseMap)
-        uint32_t smap;    // the sub-chunk's PhaseMap
-        uint32_t sfirst;  // first natural head in the sub-chunk (kNone: none)
-    };
+    }
+
     // sub-chunk s (in pf) through the wave's LDS image; p_sub = the byte before
     // it; pf_next: load sub-chunk s+1 into pf once this one is in LDS. Returns
     // the sub-chunk's last byte (uniform).
-    auto scan_sub = [&](int s, Sub &L, u32x4 (&pf)[NJ], uint32_t p_sub, bool pf_next) -> uint32_t {
-        const uint64_t so = chunk_off + (uint64_t)s * WB;
+    __device__ uint32_t scan_sub(uint64_t off, int s, Sub &L, u32x4 (&pf)[NJ], uint32_t p_sub, bool pf_next) const
+    {
+        const uint64_t so = off + (uint64_t)s * WB;
 #pragma unroll
         for (int j = 0; j < NJ; ++j)
             *reinterpret_cast<u32x4 *>(img + j * 1024 + lane * 16) = pf[j];
         if (pf_next)
-            load_sub(s + 1, pf);  // lands while this sub-chunk is scanned
+            load_sub(off, s + 1, pf);  // lands while this sub-chunk is scanned
         const uint64_t lane_off = so + o;
         L.vbl = lane_off >= n ? 0u : (n - lane_off >= LB ? (uint32_t)LB : (uint32_t)(n - lane_off));
         u32x4 x[CH];
@@ -466,8 +506,10 @@ __global__ __launch_bounds__(T) void rl_encode_wave_kernel(
         const uint32_t ff = (uint32_t)__shfl(L.fpos, fl, kWave);
         L.sfirst = hb ? (uint32_t)fl * LB + ff : kNone;
         return (uint32_t)__builtin_amdgcn_readlane((int)mylast, kWave - 1);
-    };
-    auto head_masks = [&](const Sub &L, uint32_t c0, bool with_split, uint64_t &h0, uint64_t &h1) {
+    }
+
+    __device__ void head_masks(const Sub &L, uint32_t c0, bool with_split, uint64_t &h0, uint64_t &h1) const
+    {
         const uint32_t j0 = c0 == 0 ? 0u : 255u - c0;
         const bool split = with_split && j0 < L.fpos && j0 < L.vbl;
         h0 = h1 = 0;
@@ -481,12 +523,13 @@ __global__ __launch_bounds__(T) void rl_encode_wave_kernel(
             else
                 h1 |= (uint64_t)h << (16 * (c - 4));
         }
-    };
+    }
+
     // a lane's runs from its head masks: head h ends the run before it (count =
     // h - previous head, or c_first + h for the lane's first head, 255 for 0;
     // value = the byte before h), records at slot, slot + 1, ...
-    auto lane_runs = [&](const Sub &L, uint64_t h0, uint64_t h1, uint32_t c_first, uint8_t *sc, uint8_t *sv,
-                         uint32_t slot) {
+    __device__ void lane_runs(const Sub &L, uint64_t h0, uint64_t h1, uint32_t c_first, uint32_t slot) const
+    {
         int prev = -1;
         uint32_t val = L.p0;
         while (h0 | h1) {
@@ -502,73 +545,277 @@ __global__ __launch_bounds__(T) void rl_encode_wave_kernel(
             cnt = cnt == 0 ? 255u : cnt;
             const uint32_t q = (uint32_t)pos;
             const uint32_t nval = my[(((q >> 4) ^ sw) * 16) + (q & 15u)];
-            sc[slot] = (uint8_t)cnt;
-            sv[slot] = (uint8_t)val;
+            stc[slot] = (uint8_t)cnt;
+            stv[slot] = (uint8_t)val;
             val = nval;
             ++slot;
             prev = pos;
         }
-    };
-
-    // ---- this wave's chunk: stage the state-independent runs ----------------
-    u32x4 pf[NJ];
-    uint32_t p_sub = 0, v0 = 0;
-    if (ns > 0) {
-        load_sub(0, pf);
-        p_sub = chunk_off > 0 ? (uint32_t)in[chunk_off - 1] : 0u;
     }
-    uint32_t rel_in = kMapIdent;   // PhaseMap from the chunk start to this sub-chunk
-    uint32_t first = kNone;        // the chunk's first natural head (chunk-relative)
-    uint32_t K = 0;                // state-independent heads so far
-    int nst = SUB;                 // sub-chunks whose runs are all staged
-    uint32_t Kst = 0, rel_st = kMapIdent;
-    for (int s = 0; s < ns; ++s) {
-        Sub L;
-        const uint32_t last = scan_sub(s, L, pf, p_sub, s + 1 < ns);
-        if (s == 0)
-            v0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)img[0]);
-        p_sub = last;
-        const bool seen = first != kNone;
-        const uint32_t lrel = pm_compose(rel_in, L.lrel);
-        bool lane_indep = false, after = false;
-        if (seen) {
-            lane_indep = after = true;
-        } else if (L.sfirst != kNone && o + LB > L.sfirst) {
-            lane_indep = true;
-            after = o > L.sfirst;
+
+    // The staging pass over the chunk at `off` (`len` bytes): every sub-chunk's
+    // PhaseMap and natural heads; the runs of the state-independent heads are
+    // staged in LDS (stc/stv) at their chunk-local index until the staging area
+    // is full (nst: the sub-chunks staged completely).
+    template <class Hook>
+    __device__ void scan_chunk(uint64_t off, uint32_t len, Chunk &C, Hook &&hook) const
+    {
+        C.off = off;
+        C.len = len;
+        C.ns = (int)((len + WB - 1) / WB);
+        u32x4 pf[NJ];
+        uint32_t p_sub = 0;
+        C.v0 = 0;
+        if (C.ns > 0) {
+            load_sub(off, 0, pf);
+            p_sub = off > 0 ? (uint32_t)in[off - 1] : 0u;
         }
-        const uint32_t cr = after ? pm_apply(lrel, 1) : 0u;  // constant after the first head
-        uint64_t h0 = 0, h1 = 0;
-        uint32_t indep = 0;
-        if (lane_indep) {
-            head_masks(L, cr, after, h0, h1);
-            indep = (uint32_t)(__popcll(h0) + __popcll(h1));
+        uint32_t rel_in = kMapIdent;  // PhaseMap from the chunk start to this sub-chunk
+        uint32_t first = kNone;
+        uint32_t K = 0;
+        int nst = SUB;
+        uint32_t Kst = 0, rel_st = kMapIdent;
+        for (int s = 0; s < C.ns; ++s) {
+            Sub L;
+            const uint32_t last = scan_sub(off, s, L, pf, p_sub, s + 1 < C.ns);
+            if (s == 0)
+                C.v0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)img[0]);
+            p_sub = last;
+            const bool seen = first != kNone;
+            const uint32_t lrel = pm_compose(rel_in, L.lrel);
+            bool lane_indep = false, after = false;
+            if (seen) {
+                lane_indep = after = true;
+            } else if (L.sfirst != kNone && o + LB > L.sfirst) {
+                lane_indep = true;
+                after = o > L.sfirst;
+            }
+            const uint32_t cr = after ? pm_apply(lrel, 1) : 0u;  // constant after the first head
+            uint64_t h0 = 0, h1 = 0;
+            uint32_t indep = 0;
+            if (lane_indep) {
+                head_masks(L, cr, after, h0, h1);
+                indep = (uint32_t)(__popcll(h0) + __popcll(h1));
+            }
+            const uint32_t hincl = wave_incl_scan_u32(indep);
+            const uint32_t ks = (uint32_t)__builtin_amdgcn_readlane((int)hincl, kWave - 1);
+            if (nst == SUB && K + ks > (uint32_t)SW) {  // wave-uniform
+                nst = s;
+                Kst = K;
+                rel_st = rel_in;
+            }
+            const uint32_t slot = K + (hincl - indep);
+            if (!seen && L.sfirst != kNone)
+                first = (uint32_t)s * WB + L.sfirst;
+            K += ks;
+            rel_in = pm_compose(rel_in, L.smap);
+            if (nst == SUB && indep && !(FLRL_RL_ABL & 4))
+                lane_runs(L, h0, h1, cr, slot);
+            hook(s);
         }
-        const uint32_t hincl = wave_incl_scan_u32(indep);
-        const uint32_t ks = (uint32_t)__builtin_amdgcn_readlane((int)hincl, kWave - 1);
-        if (nst == SUB && K + ks > (uint32_t)SW) {  // wave-uniform
-            nst = s;
+        if (nst >= C.ns) {
+            nst = C.ns;
             Kst = K;
             rel_st = rel_in;
         }
-        const uint32_t slot = K + (hincl - indep);
-        if (!seen && L.sfirst != kNone)
-            first = (uint32_t)s * WB + L.sfirst;
-        K += ks;
-        rel_in = pm_compose(rel_in, L.smap);
-        if (nst == SUB && indep && !(FLRL_RL_ABL & 4))
-            lane_runs(L, h0, h1, cr, stc, stv, slot);
+        C.nst = nst;
+        C.first = first;
+        C.K = K;
+        C.Kst = Kst;
+        C.rel_in = rel_in;
+        C.rel_st = rel_st;
     }
-    if (nst >= ns) {
-        nst = ns;
-        Kst = K;
-        rel_st = rel_in;
-    }
-    const uint32_t pre = first != kNone ? first : chunk_len;
 
+    // Staged records to / from a global slot (16-byte vectors; this wave's own).
+    __device__ void staging_to(uint8_t *gc, uint8_t *gv, uint32_t K) const
+    {
+        for (uint32_t j = (uint32_t)lane * 16; j < K; j += kWave * 16) {
+            *reinterpret_cast<u32x4 *>(gc + j) = *reinterpret_cast<const u32x4 *>(stc + j);
+            *reinterpret_cast<u32x4 *>(gv + j) = *reinterpret_cast<const u32x4 *>(stv + j);
+        }
+    }
+    __device__ void staging_from(const uint8_t *gc, const uint8_t *gv, uint32_t K) const
+    {
+        constexpr int R = (SW + kWave * 16 - 1) / (kWave * 16);
+        u32x4 a[R], b[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {  // all loads in flight, then the LDS writes
+            const uint32_t j = (uint32_t)(r * kWave + lane) * 16;
+            if (j < K) {
+                a[r] = *reinterpret_cast<const u32x4 *>(gc + j);
+                b[r] = *reinterpret_cast<const u32x4 *>(gv + j);
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const uint32_t j = (uint32_t)(r * kWave + lane) * 16;
+            if (j < K) {
+                *reinterpret_cast<u32x4 *>(stc + j) = a[r];
+                *reinterpret_cast<u32x4 *>(stv + j) = b[r];
+            }
+        }
+    }
+
+    // Emission of chunk C with the state (heads before it, chunk state) at its
+    // start; its staged records are in stc/stv. The wave whose chunk ends the
+    // input also writes the final run and R.
+    __device__ void emit(const Chunk &C, uint64_t h_in, uint32_t c_in, uint8_t *__restrict__ counts,
+                         uint8_t *__restrict__ values, uint64_t *__restrict__ runs_out) const
+    {
+        if (C.ns == 0 || (FLRL_RL_ABL & 2))
+            return;
+        const uint32_t pre = C.pre();
+        {
+            // staged sub-chunks [0, nst): split heads h_in + j end full 255-byte
+            // chunks of the chunk's first byte, then the staged records
+            const uint32_t st_len = (uint32_t)C.nst * WB;
+            const uint32_t S_st = splits(c_in, pre < st_len ? pre : st_len);
+            for (uint32_t j = (uint32_t)lane; j < S_st; j += kWave) {
+                const uint64_t gi = h_in + j;
+                if (gi > 0) {
+                    counts[gi - 1] = 255;
+                    values[gi - 1] = (uint8_t)C.v0;
+                }
+            }
+            const uint64_t g0 = h_in + S_st;  // global index of the first natural head
+            if (C.Kst) {
+                if (lane == 0 && g0 > 0) {
+                    const uint32_t c = add_c(c_in, C.first);
+                    counts[g0 - 1] = (uint8_t)(c == 0 ? 255u : c);
+                    values[g0 - 1] = stv[0];
+                }
+                for (uint32_t j = 1 + (uint32_t)lane; j < C.Kst; j += kWave) {
+                    counts[g0 + j - 1] = stc[j];
+                    values[g0 + j - 1] = stv[j];
+                }
+            }
+        }
+        if (C.nst < C.ns) {
+            // sub-chunks [nst, ns): re-read and emit with the true states
+            uint32_t rel = C.rel_st;
+            uint64_t hb = h_in + splits(c_in, pre < (uint32_t)C.nst * WB ? pre : (uint32_t)C.nst * WB) + C.Kst;
+            const uint64_t re_off = C.off + (uint64_t)C.nst * WB;
+            uint32_t pb = re_off > 0 ? (uint32_t)in[re_off - 1] : 0u;
+            u32x4 pf[NJ];
+            load_sub(C.off, C.nst, pf);
+            for (int s = C.nst; s < C.ns; ++s) {
+                // the staged copy-out above and the previous sub-chunk's reads of the
+                // staging and the image are this wave's own LDS ops: in order
+                Sub L;
+                pb = scan_sub(C.off, s, L, pf, pb, s + 1 < C.ns);
+                const uint32_t c_lane = pm_apply(pm_compose(rel, L.lrel), c_in);
+                uint64_t hm0, hm1;
+                head_masks(L, c_lane, true, hm0, hm1);
+                const uint32_t hl = (uint32_t)(__popcll(hm0) + __popcll(hm1));
+                const uint32_t hincl = wave_incl_scan_u32(hl);
+                const uint32_t hs = (uint32_t)__builtin_amdgcn_readlane((int)hincl, kWave - 1);
+                const uint64_t g = hb + (hincl - hl);
+                if (hs <= (uint32_t)SW) {
+                    // sparse: stage at (g - hb), store contiguously
+                    lane_runs(L, hm0, hm1, c_lane, (uint32_t)(g - hb));
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                    for (uint32_t j = lane; j < hs; j += kWave) {
+                        const uint64_t gi = hb + j;
+                        if (gi > 0) {
+                            counts[gi - 1] = stc[j];
+                            values[gi - 1] = stv[j];
+                        }
+                    }
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                } else {
+                    // dense: ONE lane row at a time, lane t taking byte positions t
+                    // and 64 + t of the row (ranks by popcount): contiguous stores
+                    const uint64_t below = ((uint64_t)1 << lane) - 1;
+#pragma unroll 1
+                    for (int r = 0; r < kWave; ++r) {
+                        const uint64_t h0 = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(hm0 >> 32), r) << 32) |
+                                            (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)hm0, r);
+                        const uint64_t h1 = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(hm1 >> 32), r) << 32) |
+                                            (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)hm1, r);
+                        const uint64_t g_row = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(g >> 32), r) << 32) |
+                                               (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)g, r);
+                        const uint32_t c_row = (uint32_t)__builtin_amdgcn_readlane((int)c_lane, r);
+                        const uint32_t p_row = (uint32_t)__builtin_amdgcn_readlane((int)L.p0, r);
+                        const uint32_t rr = (uint32_t)r;
+                        const uint8_t *rowp = img + rr * LB;
+#pragma unroll
+                        for (int half = 0; half < CH / 4; ++half) {
+                            const uint64_t hm = half ? h1 : h0;
+                            if ((hm >> lane) & 1u) {
+                                const uint64_t bl = hm & below;
+                                const uint32_t pos = (uint32_t)(half * 64 + lane);
+                                const uint32_t rank = (half ? (uint32_t)__popcll(h0) : 0u) + (uint32_t)__popcll(bl);
+                                int prev;
+                                if (bl)
+                                    prev = half * 64 + 63 - __builtin_clzll(bl);
+                                else
+                                    prev = (half && h0) ? 63 - __builtin_clzll(h0) : -1;
+                                uint32_t cnt = prev < 0 ? add_c(c_row, pos) : pos - (uint32_t)prev;
+                                cnt = cnt == 0 ? 255u : cnt;
+                                const uint32_t q = pos - 1;
+                                const uint32_t val = pos == 0 ? p_row : rowp[(((q >> 4) ^ swz(rr)) * 16) + (q & 15u)];
+                                const uint64_t gi = g_row + rank;
+                                if (gi > 0) {
+                                    counts[gi - 1] = (uint8_t)cnt;
+                                    values[gi - 1] = (uint8_t)val;
+                                }
+                            }
+                        }
+                    }
+                }
+                hb += hs;
+                rel = pm_compose(rel, L.smap);
+            }
+        }
+        // the final run (ends at byte n-1): the wave whose chunk holds it
+        if (C.off + C.len == n && lane == 0) {
+            const uint64_t R = h_in + splits(c_in, pre) + C.K;
+            const uint32_t c_end = pm_apply(C.rel_in, c_in);
+            counts[R - 1] = (uint8_t)(c_end == 0 ? 255u : c_end);
+            values[R - 1] = in[n - 1];
+            *runs_out = R;
+        }
+    }
+};
+
+// One tile per workgroup (grid = tiles), in ticket order: stage, publish the
+// tile map, ONE look-back by wave 0 while waves 1-3 wait, emit. Three block
+// barriers per tile (ticket, wave maps, state).
+template <int T, int LB, int SUB>
+__global__ __launch_bounds__(T) void rl_encode_wave_kernel(
+    const uint8_t *__restrict__ in, uint64_t n, uint32_t ntiles, uint8_t *__restrict__ counts,
+    uint8_t *__restrict__ values, uint64_t *__restrict__ runs_out, Ctrl *ctrl, uint64_t *status)
+{
+    constexpr int W = T / kWave;
+    using Wv = RlWave<LB, SUB, W>;
+    __shared__ __attribute__((aligned(16))) uint8_t s_lds[W * Wv::WB + kRlStageBytes];
+    __shared__ uint64_t s_map[W];
+    __shared__ uint64_t s_st[W];
+    __shared__ uint32_t s_ticket;
+
+    const int tid = threadIdx.x;
+    const int w = tid / kWave;
+    const Wv V(in, n, s_lds, w);
+    const uint32_t tile = take_ticket(ctrl, &s_ticket);
+    if (tile >= ntiles) {  // the scratch's ticket was not reset for this launch
+        if (threadIdx.x == 0)
+            raise_error(ctrl, FLRL_E_ARG);
+        return;
+    }
+    FLRL_RL_TRACE(tile, 0);
+    typename Wv::Chunk C;
+    {
+        const uint64_t off = (uint64_t)tile * Wv::TBT + (uint64_t)w * Wv::CB;
+        const uint32_t len = off >= n ? 0u : (n - off < (uint64_t)Wv::CB ? (uint32_t)(n - off) : (uint32_t)Wv::CB);
+        V.scan_chunk(off, len, C, [](int) {});
+    }
     // ---- the wave maps -> the tile's map -> ONE look-back -> each wave's state
-    if (lane == 0)
-        s_map[w] = first != kNone ? sm_nat(first, K, rel_in & 0xFFu) : sm_nonat(chunk_len);
+    if (V.lane == 0)
+        s_map[w] = C.map();
     __syncthreads();
     FLRL_RL_TRACE(tile, 1);
     if (w == 0) {
@@ -577,6 +824,8 @@ __global__ __launch_bounds__(T) void rl_encode_wave_kernel(
         for (int v = 1; v < W; ++v)
             tmap = sm_compose(tmap, s_map[v]);
         uint64_t st;
+        if (FLRL_RL_LB_PRIO)
+            __builtin_amdgcn_s_setprio(FLRL_RL_LB_PRIO);
         if (FLRL_RL_ABL & 1) {
             st = sm_const((uint64_t)tile * 4096u, 0);
         } else {
@@ -585,7 +834,9 @@ __global__ __launch_bounds__(T) void rl_encode_wave_kernel(
             st = lookback_seg<kRlLookG>(status, tile, tmap, ctrl);
             FLRL_RL_TRACE(tile, 3);
         }
-        if (lane == 0) {
+        if (FLRL_RL_LB_PRIO)
+            __builtin_amdgcn_s_setprio(0);
+        if (V.lane == 0) {
 #pragma unroll
             for (int v = 0; v < W; ++v) {
                 s_st[v] = st;
@@ -594,125 +845,8 @@ __global__ __launch_bounds__(T) void rl_encode_wave_kernel(
         }
     }
     __syncthreads();
-    if (ns == 0 || (FLRL_RL_ABL & 2))
-        return;
-    const uint64_t h_in = sm_h(s_st[w]);
-    const uint32_t c_in = sm_c(s_st[w]);
-    {
-        // staged sub-chunks [0, nst): split heads h_in + j end full 255-byte
-        // chunks of the chunk's first byte, then the staged records
-        const uint32_t st_len = (uint32_t)nst * WB;
-        const uint32_t S_st = splits(c_in, pre < st_len ? pre : st_len);
-        for (uint32_t j = (uint32_t)lane; j < S_st; j += kWave) {
-            const uint64_t gi = h_in + j;
-            if (gi > 0) {
-                counts[gi - 1] = 255;
-                values[gi - 1] = (uint8_t)v0;
-            }
-        }
-        const uint64_t g0 = h_in + S_st;  // global index of the first natural head
-        if (Kst) {
-            if (lane == 0 && g0 > 0) {
-                const uint32_t c = add_c(c_in, first);
-                counts[g0 - 1] = (uint8_t)(c == 0 ? 255u : c);
-                values[g0 - 1] = stv[0];
-            }
-            for (uint32_t j = 1 + (uint32_t)lane; j < Kst; j += kWave) {
-                counts[g0 + j - 1] = stc[j];
-                values[g0 + j - 1] = stv[j];
-            }
-        }
-    }
-    if (nst < ns) {
-        // sub-chunks [nst, ns): re-read and emit with the true states
-        uint32_t rel = rel_st;
-        uint64_t hb = h_in + splits(c_in, pre < (uint32_t)nst * WB ? pre : (uint32_t)nst * WB) + Kst;
-        const uint64_t re_off = chunk_off + (uint64_t)nst * WB;
-        uint32_t pb = re_off > 0 ? (uint32_t)in[re_off - 1] : 0u;
-        load_sub(nst, pf);
-        for (int s = nst; s < ns; ++s) {
-            // the staged copy-out above and the previous sub-chunk's reads of the
-            // staging and the image are this wave's own LDS ops: in order
-            Sub L;
-            pb = scan_sub(s, L, pf, pb, s + 1 < ns);
-            const uint32_t c_lane = pm_apply(pm_compose(rel, L.lrel), c_in);
-            uint64_t hm0, hm1;
-            head_masks(L, c_lane, true, hm0, hm1);
-            const uint32_t hl = (uint32_t)(__popcll(hm0) + __popcll(hm1));
-            const uint32_t hincl = wave_incl_scan_u32(hl);
-            const uint32_t hs = (uint32_t)__builtin_amdgcn_readlane((int)hincl, kWave - 1);
-            const uint64_t g = hb + (hincl - hl);
-            if (hs <= (uint32_t)SW) {
-                // sparse: stage at (g - hb), store contiguously
-                lane_runs(L, hm0, hm1, c_lane, stc, stv, (uint32_t)(g - hb));
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                for (uint32_t j = lane; j < hs; j += kWave) {
-                    const uint64_t gi = hb + j;
-                    if (gi > 0) {
-                        counts[gi - 1] = stc[j];
-                        values[gi - 1] = stv[j];
-                    }
-                }
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            } else {
-                // dense: ONE lane row at a time, lane t taking byte positions t
-                // and 64 + t of the row (ranks by popcount): contiguous stores
-                const uint64_t below = ((uint64_t)1 << lane) - 1;
-#pragma unroll 1
-                for (int r = 0; r < kWave; ++r) {
-                    const uint64_t h0 = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(hm0 >> 32), r) << 32) |
-                                        (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)hm0, r);
-                    const uint64_t h1 = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(hm1 >> 32), r) << 32) |
-                                        (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)hm1, r);
-                    const uint64_t g_row = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(g >> 32), r) << 32) |
-                                           (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)g, r);
-                    const uint32_t c_row = (uint32_t)__builtin_amdgcn_readlane((int)c_lane, r);
-                    const uint32_t p_row = (uint32_t)__builtin_amdgcn_readlane((int)L.p0, r);
-                    const uint32_t rr = (uint32_t)r;
-                    const uint8_t *rowp = img + rr * LB;
-#pragma unroll
-                    for (int half = 0; half < CH / 4; ++half) {
-                        const uint64_t hm = half ? h1 : h0;
-                        if ((hm >> lane) & 1u) {
-                            const uint64_t bl = hm & below;
-                            const uint32_t pos = (uint32_t)(half * 64 + lane);
-                            const uint32_t rank = (half ? (uint32_t)__popcll(h0) : 0u) + (uint32_t)__popcll(bl);
-                            int prev;
-                            if (bl)
-                                prev = half * 64 + 63 - __builtin_clzll(bl);
-                            else
-                                prev = (half && h0) ? 63 - __builtin_clzll(h0) : -1;
-                            uint32_t cnt = prev < 0 ? add_c(c_row, pos) : pos - (uint32_t)prev;
-                            cnt = cnt == 0 ? 255u : cnt;
-                            const uint32_t q = pos - 1;
-                            const uint32_t val = pos == 0 ? p_row : rowp[(((q >> 4) ^ swz(rr)) * 16) + (q & 15u)];
-                            const uint64_t gi = g_row + rank;
-                            if (gi > 0) {
-                                counts[gi - 1] = (uint8_t)cnt;
-                                values[gi - 1] = (uint8_t)val;
-                            }
-                        }
-                    }
-                }
-            }
-            hb += hs;
-            rel = pm_compose(rel, L.smap);
-        }
-    }
-
+    V.emit(C, sm_h(s_st[w]), sm_c(s_st[w]), counts, values, runs_out);
     FLRL_RL_TRACE(tile, 4);
-    // ---- the final run (ends at byte n-1): the wave whose chunk holds it ----
-    if (chunk_off + chunk_len == n && lane == 0) {
-        const uint64_t R = h_in + splits(c_in, pre) + K;
-        const uint32_t c_end = pm_apply(rel_in, c_in);
-        counts[R - 1] = (uint8_t)(c_end == 0 ? 255u : c_end);
-        values[R - 1] = in[n - 1];
-        *runs_out = R;
-    }
 }
 
 // ---- decode pre-pass: output offsets of each decode tile ------------------
@@ -1073,11 +1207,12 @@ __global__ __launch_bounds__(kRdThreads) void rl_decode_kernel(
 
 
 struct RlEncLayout {
-    size_t tiles, bytes;
+    size_t tiles, zero, bytes;
     explicit RlEncLayout(size_t n)
     {
         tiles = div_up(n, (size_t)kRlTileBytes);
-        bytes = sizeof(Ctrl) + round_up(tiles * 8, 16);
+        zero = sizeof(Ctrl) + round_up(tiles * 8, 16);  // ticket, error, status granules
+        bytes = zero;
     }
 };
 
@@ -1115,7 +1250,7 @@ extern "C" int flrl_rl_encode_device(const uint8_t *d_in, size_t n, uint8_t *d_c
                          scratch_bytes, L.bytes);
     if (!aligned16(d_scratch))
         return set_error(FLRL_E_ARG, "flrl_rl_encode_device: scratch not 16-byte aligned");
-    FLRL_HIP(scratch_reset(d_scratch, L.bytes, s));
+    FLRL_HIP(scratch_reset(d_scratch, L.zero, s));
     if (n == 0) {
         FLRL_HIP(zero_async(d_runs, sizeof(uint64_t), s));
         return FLRL_OK;

@@ -5,7 +5,9 @@ import sys
 
 import numpy as np
 
-t = np.fromfile(sys.argv[1], dtype=np.uint64).reshape(-1, 8)[:, :5].astype(np.int64)
+raw = np.fromfile(sys.argv[1], dtype=np.uint64).reshape(-1, 8)
+t = raw[:, :5].astype(np.int64)
+spins, rounds = raw[:, 5].astype(np.int64), raw[:, 6].astype(np.int64)
 t0 = t[t > 0].min()
 t = (t - t0) * 10 / 1000.0  # us
 start, scanned, pub, lb, end = t[:, 0], t[:, 1], t[:, 2], t[:, 3], t[:, 4]
@@ -25,6 +27,8 @@ pct(pub[1:] - pub[:-1], "pub[t] - pub[t-1]")
 print("fraction of tiles whose predecessor published later:", round(float((pub[:-1] > pub[1:]).mean()), 3))
 pct(lb[1:] - lb[:-1], "lb[t] - lb[t-1]")
 i = len(t) // 2
+print("look-back spins: mean", round(float(spins.mean()), 2), "p90", int(np.percentile(spins, 90)),
+      "| windows: mean", round(float(rounds.mean()), 2), "p90", int(np.percentile(rounds, 90)), "max", int(rounds.max()))
 busy = np.zeros(int(end.max()) + 2)
 for a, b in zip(start, end):  # tiles in flight per us
     busy[int(a):int(b) + 1] += 1

@@ -51,6 +51,13 @@ __device__ __forceinline__ uint64_t rl_rtime()
         if (threadIdx.x == 0)                                                    \
             g_trace[(uint64_t)(tile) * 8 + (k)] = rl_rtime(); \
     } while (0)
+#define FLRL_RL_LB_STAT(tile, spins, rounds)                                      \
+    do {                                                                          \
+        if ((threadIdx.x & 63) == 0) {                                            \
+            g_trace[(uint64_t)(tile) * 8 + 5] = (spins);                           \
+            g_trace[(uint64_t)(tile) * 8 + 6] = (rounds);                          \
+        }                                                                         \
+    } while (0)
 #endif
 #include "flrl_common.hip"
 #include "flrl_rl.hip"
