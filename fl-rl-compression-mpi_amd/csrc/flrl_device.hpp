@@ -65,12 +65,39 @@ __device__ __forceinline__ uint32_t take_ticket(Ctrl *c, uint32_t *s_slot)
     return *s_slot;
 }
 
+// u64 moves between lanes without the LDS crossbar: DPP from a higher (row_shl)
+// or lower (row_shr) lane within 16-lane rows (lanes without a source read 0),
+// and a wave-uniform read of one lane.
+template <int CTRL>
+__device__ __forceinline__ uint64_t dpp64_0(uint64_t v)
+{
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)v, CTRL, 0xF, 0xF, true);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(v >> 32), CTRL, 0xF, 0xF, true);
+    return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, int l)
+{
+    return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l) << 32) |
+           (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+}
+
+// Sum over the wave (wave-uniform result): four DPP row_shr steps leave each
+// 16-lane row's sum in its lane 15, then the four row sums are added. (Six
+// xor-butterfly shuffles were twelve dependent LDS-crossbar round trips.)
 __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v)
 {
+#ifdef FLRL_SUM_XOR  // A/B builds only
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1)
         v += __shfl_xor(v, o, kWave);
     return v;
+#else
+    v += dpp64_0<0x111>(v);
+    v += dpp64_0<0x112>(v);
+    v += dpp64_0<0x114>(v);
+    v += dpp64_0<0x118>(v);
+    return readlane64(v, 15) + readlane64(v, 31) + readlane64(v, 47) + readlane64(v, 63);
+#endif
 }
 
 // OR across each aligned group of 8 lanes with DPP (no LDS crossbar):

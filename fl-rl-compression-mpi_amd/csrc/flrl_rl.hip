@@ -217,21 +217,6 @@ __device__ __forceinline__ void publish_seg(uint64_t *status, uint32_t tile, uin
                                                : (kFlagA | map));
 }
 
-// DPP move of a u64 from a higher lane (row_shl:k within 16-lane rows; lanes
-// without a source read 0) and a wave-uniform read of a lane's u64.
-template <int CTRL>
-__device__ __forceinline__ uint64_t dpp_dn64(uint64_t v)
-{
-    const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)v, CTRL, 0xF, 0xF, true);
-    const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(v >> 32), CTRL, 0xF, 0xF, true);
-    return ((uint64_t)hi << 32) | lo;
-}
-__device__ __forceinline__ uint64_t readlane64(uint64_t v, int l)
-{
-    return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l) << 32) |
-           (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
-}
-
 template <int G>
 __device__ __forceinline__ uint64_t lookback_seg(uint64_t *status, uint32_t tile, uint64_t map,
                                                  Ctrl *ctrl)
@@ -293,10 +278,10 @@ __device__ __forceinline__ uint64_t lookback_seg(uint64_t *status, uint32_t tile
         // composition of the window, oldest first (identity: no-nat L 0 = 0):
         // four DPP row_shl steps compose each 16-lane row into its lane 0 (lanes
         // past a row read 0), then the four row results are composed
-        m = sm_compose(dpp_dn64<0x101>(m), m);
-        m = sm_compose(dpp_dn64<0x102>(m), m);
-        m = sm_compose(dpp_dn64<0x104>(m), m);
-        m = sm_compose(dpp_dn64<0x108>(m), m);
+        m = sm_compose(dpp64_0<0x101>(m), m);
+        m = sm_compose(dpp64_0<0x102>(m), m);
+        m = sm_compose(dpp64_0<0x104>(m), m);
+        m = sm_compose(dpp64_0<0x108>(m), m);
         const uint64_t win = sm_compose(sm_compose(sm_compose(readlane64(m, 48), readlane64(m, 32)),
                                                    readlane64(m, 16)),
                                         readlane64(m, 0));
