@@ -1038,16 +1038,20 @@ __global__ __launch_bounds__(kRdThreads) void rl_decode_kernel(
                 }
                 __syncthreads();
                 const uint32_t wlen = (uint32_t)(cend - g0);
+                // whole chunks from 16-byte stores; the (at most two) chunks shared with
+                // the neighbouring tiles byte by byte, one byte per lane of waves 0 and 1
+                // (one thread looping over them held the other waves at the next barrier)
                 for (uint32_t ch = tid; ch * 16 < wlen; ch += T) {
                     const uint64_t gp = g0 + 16ull * ch;
-                    const u32x4 o = s_big4[ch];
-                    if (gp >= cbase && gp + 16 <= cend) {
-                        *reinterpret_cast<u32x4 *>(out + gp) = o;  // plain: see the note above
-                    } else {
-                        for (uint32_t f = 0; f < 16; ++f)
-                            if (gp + f >= cbase && gp + f < cend)
-                                out[gp + f] = (uint8_t)(o[f >> 2] >> (8 * (f & 3)));
-                    }
+                    if (gp >= cbase && gp + 16 <= cend)
+                        *reinterpret_cast<u32x4 *>(out + gp) = s_big4[ch];  // plain: see the note above
+                }
+                if (wave < 2 && lane < 16) {
+                    const uint32_t ch = wave == 0 ? 0u : (wlen - 1) / 16;
+                    const uint64_t gp = g0 + 16ull * ch + (uint64_t)lane;
+                    const bool edge = wave == 0 ? cbase > g0 || cend - g0 < 16 : (wlen & 15) != 0 && ch > 0;
+                    if (edge && gp >= cbase && gp < cend)
+                        out[gp] = reinterpret_cast<const uint8_t *>(s_big4)[16 * ch + lane];
                 }
             } else {
             {
