@@ -352,6 +352,26 @@ __device__ __forceinline__ u32x4 load16_tail(const uint8_t *p, uint64_t o, uint6
     return v;
 }
 
+// Branch-free pieces of load16_tail for software pipelines: the load itself
+// with its address clamped to the last 16-byte block of [0, n) (n >= 1; every
+// lane issues exactly one load and no wait, so the compiler can count the
+// loads in flight across it), and the masking, applied when the data is used:
+// bytes at or past n read as zero.
+__device__ __forceinline__ u32x4 load16_clamped(const uint8_t *p, uint64_t o, uint64_t n)
+{
+    const uint64_t last = (n - 1) & ~15ull;
+    return *reinterpret_cast<const u32x4 *>(p + (o < last ? o : last));
+}
+__device__ __forceinline__ uint32_t valid16(uint64_t o, uint64_t n)
+{
+    return o >= n ? 0u : (n - o >= 16 ? 16u : (uint32_t)(n - o));
+}
+__device__ __forceinline__ uint32_t mask_dword(uint32_t x, uint32_t valid, int d)
+{
+    const uint32_t vb = valid > 4u * d ? valid - 4u * d : 0u;
+    return vb >= 4 ? x : x & ((1u << (8 * vb)) - 1u);
+}
+
 // 16-byte store of v to bytes [o, o+16) of p, dropping bytes at or past n.
 __device__ __forceinline__ void store16_tail(uint8_t *p, uint64_t o, uint64_t n, u32x4 v)
 {

@@ -34,6 +34,7 @@
 // into an LDS byte window instead. Chunks a tile shares with its neighbours are
 // written byte by byte.
 #include <hip/hip_runtime.h>
+#include <algorithm>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -88,9 +89,6 @@ constexpr int kRlStageBytes = FLRL_RL_STAGE;  // LDS run staging per workgroup
 constexpr int kRdRuns = 4096;        // runs per decode tile
 constexpr int kRdThreads = 256;
 constexpr int kRdPerCU = 4;          // resident decode workgroups per CU (LDS 37 KB each)
-constexpr int kRoRunsPerThread = 256;
-constexpr int kRoRuns = kRoRunsPerThread * kThreads;  // runs per offsets workgroup
-static_assert(kRdRuns % kRoRunsPerThread == 0, "whole offsets lanes per decode tile");
 
 // ---- PhaseMap packed in a u32: bit 8 = constant, bits 0-7 = value (< 255) ----
 constexpr uint32_t kMapIdent = 0;
@@ -835,15 +833,43 @@ __global__ __launch_bounds__(T) void rl_encode_wave_kernel(
 }
 
 // ---- decode pre-pass: output offsets of each decode tile ------------------
-// `iters` rounds of kRoRuns counts per workgroup; offsets are written
-// workgroup-relative, then the workgroup's base (block_prefix_all) is added.
-__global__ __launch_bounds__(kThreads) void rl_offsets_kernel(
+// A workgroup (4 waves) takes a contiguous span of iters x kRoRuns counts by
+// ticket; wave w owns the w-th quarter of it and walks it in steps of 16384
+// counts with no block barrier (waves overlap each other's loads), each step
+// loaded coalesced (one load instruction = 1 KiB of consecutive counts: lane
+// l, vector q holds counts 16 (64 q + l) .. + 15) and summed into TR-run tile
+// sums by wave reductions; tile entries are written wave-relative. Then one
+// block scan of the wave totals, the workgroup's base from all predecessors
+// (block_prefix_all), and each wave adds its base to its own entries.
+// (Lane-contiguous 128- or 256-byte segments with a block barrier per round
+// ran at ~4 TB/s.)
+constexpr int kRoThreads = 256;
+constexpr int kRoWaves = kRoThreads / kWave;
+constexpr int kRoQ = 16;                                // count vectors per lane per step
+constexpr int kRoStep = kRoQ * 16 * kWave;              // counts per wave step (16384)
+constexpr int kRoRuns = kRoStep * kRoWaves;             // counts per workgroup and iteration
+
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v)
+{
+    v += dpp_up0<0x111, 0xF>(v);
+    v += dpp_up0<0x112, 0xF>(v);
+    v += dpp_up0<0x114, 0xF>(v);
+    v += dpp_up0<0x118, 0xF>(v);
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, 15) + (uint32_t)__builtin_amdgcn_readlane((int)v, 31) +
+           (uint32_t)__builtin_amdgcn_readlane((int)v, 47) + (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+
+template <int TR>  // runs per decode tile
+__global__ __launch_bounds__(kRoThreads, 4) void rl_offsets_kernel(  // 4 workgroups per CU
     const uint8_t *__restrict__ counts, uint64_t runs, uint64_t n, uint64_t *__restrict__ tile_base,
     uint32_t ntiles, uint32_t nblocks, uint32_t iters, Ctrl *ctrl, uint64_t *status)
 {
-    __shared__ uint32_t s_wave[kWaves];
+    constexpr int TPS = kRoStep / TR;  // tiles per wave step
+    constexpr int QPT = kRoQ / TPS;    // vectors per lane per tile
+    static_assert(kRoStep % TR == 0 && TPS <= kWave, "whole tiles per wave step");
     __shared__ uint32_t s_ticket;
-    __shared__ uint64_t s_red[kWaves];
+    __shared__ uint64_t s_wtot[kRoWaves];
+    __shared__ uint64_t s_red[kRoWaves];
     const int tid = threadIdx.x;
     const int lane = tid & (kWave - 1);
     const int wave = tid / kWave;
@@ -853,76 +879,95 @@ __global__ __launch_bounds__(kThreads) void rl_offsets_kernel(
             raise_error(ctrl, FLRL_E_ARG);
         return;
     }
-    constexpr int kLanesPerTile = kRdRuns / kRoRunsPerThread;
-    uint64_t local = 0;  // output bytes before this round, workgroup-relative
-    bool bad = false;
+    // this wave's span: iters steps of kRoStep counts
+    const uint64_t w0 = ((uint64_t)blk * kRoWaves + wave) * iters * (uint64_t)kRoStep;
+    uint64_t wrun = 0;  // output bytes of the wave's span so far
     uint64_t keep = 0;
+    uint32_t zacc = 0;  // SWAR flags of zero counts
     for (uint32_t it = 0; it < iters; ++it) {
-        const uint64_t r0 = ((uint64_t)blk * iters + it) * kRoRuns + (uint64_t)tid * kRoRunsPerThread;
-        // all of the lane's count loads in flight before any is used
-        constexpr int Q = kRoRunsPerThread / 16;
-        u32x4 cq[Q];
-        if (r0 + kRoRunsPerThread <= runs) {
+        const uint64_t wb = w0 + (uint64_t)it * kRoStep;
+        if (wb >= runs)
+            break;
+        u32x4 cq[kRoQ];
+        uint32_t sq[kRoQ];
+        if (wb + kRoStep <= runs) {
 #pragma unroll
-            for (int q = 0; q < Q; ++q)
-                cq[q] = *reinterpret_cast<const u32x4 *>(counts + r0 + 16 * q);
-        } else {
+            for (int q = 0; q < kRoQ; ++q)
+                cq[q] = *reinterpret_cast<const u32x4 *>(counts + wb + 16 * (q * kWave + lane));
 #pragma unroll
-            for (int q = 0; q < Q; ++q)
-                cq[q] = load16_tail(counts, r0 + 16 * q, runs);
-        }
-        uint32_t sum = 0;
+            for (int q = 0; q < kRoQ; ++q) {
+                sq[q] = 0;
 #pragma unroll
-        for (int q = 0; q < Q; ++q) {
-            const uint64_t rq = r0 + 16 * q;
-            const u32x4 v = cq[q];
+                for (int d = 0; d < 4; ++d) {
+                    const uint32_t x = cq[q][d];
+                    sq[q] = __builtin_amdgcn_udot4(x, 0x01010101u, sq[q], false);
+                    zacc |= (x - 0x01010101u) & ~x & 0x80808080u;  // a zero count is malformed
+                }
+            }
+        } else {  // the last counts: bytes past them are masked off
 #pragma unroll
-            for (int d = 0; d < 4; ++d) {
-                const uint32_t x = v[d];
-                const uint32_t h = (x & 0x00FF00FFu) + ((x >> 8) & 0x00FF00FFu);
-                sum += (h & 0xFFFFu) + (h >> 16);
-                // a zero count inside [0, runs) is malformed
-                const uint32_t zero = (x - 0x01010101u) & ~x & 0x80808080u;
-                if (zero) {
-                    for (int i = 0; i < 4; ++i)
-                        bad |= rq + 4 * d + i < runs && ((x >> (8 * i)) & 0xFFu) == 0;
+            for (int q = 0; q < kRoQ; ++q)
+                cq[q] = load16_clamped(counts, wb + 16 * (q * kWave + lane), runs);
+#pragma unroll
+            for (int q = 0; q < kRoQ; ++q) {
+                sq[q] = 0;
+                const uint32_t valid = valid16(wb + 16 * (q * kWave + lane), runs);
+#pragma unroll
+                for (int d = 0; d < 4; ++d) {
+                    const uint32_t x = mask_dword(cq[q][d], valid, d);
+                    sq[q] = __builtin_amdgcn_udot4(x, 0x01010101u, sq[q], false);
+                    zacc |= mask_dword((x - 0x01010101u) & ~x & 0x80808080u, valid, d);
                 }
             }
         }
-        const uint32_t inc = wave_incl_scan_u32(sum);
-        if (it > 0)
-            __syncthreads();  // the previous round's s_wave readers are done
-        if (lane == kWave - 1)
-            s_wave[wave] = inc;
-        __syncthreads();
-        uint32_t before = 0, agg = 0;
+        // tile j of the step: vectors j QPT .. j QPT + QPT - 1 of every lane
+        uint64_t run = wrun;
 #pragma unroll
-        for (int v = 0; v < kWaves; ++v) {
-            before += v < wave ? s_wave[v] : 0u;
-            agg += s_wave[v];
+        for (int j = 0; j < TPS; ++j) {
+            uint32_t pj = 0;
+#pragma unroll
+            for (int q = j * QPT; q < (j + 1) * QPT; ++q)
+                pj += sq[q];
+            const uint32_t tsum = wave_sum_u32(pj);
+            const uint64_t tile = wb / TR + j;
+            if (lane == j && tile < ntiles) {
+                if (iters == 1)
+                    keep = run;  // one step: the entry waits in a register for the base
+                else
+                    tile_base[tile] = run;  // wave-relative; the bases are added below
+            }
+            run += tsum;
         }
-        const uint64_t tile = r0 / kRdRuns;
-        if (tid % kLanesPerTile == 0 && tile < ntiles) {
-            if (iters == 1)
-                keep = local + before + inc - sum;  // one round: the entry waits in a register for the base
-            else
-                tile_base[tile] = local + before + inc - sum;
-        }
-        local += agg;
+        wrun = run;
     }
-    if (bad)
+    if (zacc != 0)
         raise_error(ctrl, FLRL_E_FORMAT);
+    if (lane == 0)
+        s_wtot[wave] = wrun;
+    __syncthreads();
+    uint64_t wbase = 0, local = 0;
+#pragma unroll
+    for (int v = 0; v < kRoWaves; ++v) {
+        wbase += v < wave ? s_wtot[v] : 0ull;
+        local += s_wtot[v];
+    }
     // workgroup base from all predecessors (iters keeps the grid within kMaxPrefixBlocks)
-    const uint64_t base = block_prefix_all<kThreads>(status, blk, local, ctrl, s_red);
-    for (uint32_t it = 0; it < iters; ++it) {
-        const uint64_t r0 = ((uint64_t)blk * iters + it) * kRoRuns + (uint64_t)tid * kRoRunsPerThread;
-        const uint64_t tile = r0 / kRdRuns;
-        if (tid % kLanesPerTile == 0 && tile < ntiles)
-            tile_base[tile] = iters == 1 ? keep + base : tile_base[tile] + base;  // this lane's own entry
+    const uint64_t base = block_prefix_all<kRoThreads>(status, blk, local, ctrl, s_red) + wbase;
+    // this wave's entries: tiles w0 / TR .. of its span, one per lane. They were
+    // stored by other lanes of this wave: wait until those stores are done and
+    // read past the L1 (agent-scope loads).
+    const uint64_t t0 = w0 / TR, t1 = (w0 + (uint64_t)iters * kRoStep) / TR;
+    if (iters == 1) {
+        if (lane < TPS && t0 + lane < ntiles)
+            tile_base[t0 + lane] = keep + base;
+    } else {
+        __builtin_amdgcn_s_waitcnt(0);
+        for (uint64_t t = t0 + lane; t < t1 && t < ntiles; t += kWave)
+            tile_base[t] = granule_load(&tile_base[t]) + base;
     }
     if (blk + 1 == nblocks && tid == 0) {
-        tile_base[ntiles] = base + local;
-        if (base + local != n)
+        tile_base[ntiles] = base - wbase + local;
+        if (base - wbase + local != n)
             raise_error(ctrl, FLRL_E_FORMAT);
     }
 }
@@ -990,12 +1035,15 @@ __global__ __launch_bounds__(kRdThreads) void rl_decode_kernel(
     }
     u32x4 cv = load16_tail(counts, tile * kRdRuns + tid * RPT, runs);
     u32x4 vv = load16_tail(values, tile * kRdRuns + tid * RPT, runs);
-    uint64_t base = tile_base[tile], end = tile_base[tile + 1];
+    // The tile's output bounds come in by a VECTOR load (lane 0: start, lane 1:
+    // end): a uniform scalar load of them counts in lgkmcnt, so every LDS wait
+    // of the tile would also wait for that HBM round trip.
+    uint64_t tbv = tile_base[tile + (lane & 1)];
     for (;;) {
         const uint64_t next = tile + gridDim.x;
         __syncthreads();  // the previous tile's LDS readers are done
-        const bool skip = end > n || base >= end;  // empty, or malformed (flagged by rl_offsets_kernel)
-        const uint64_t cbase = base, cend = end;
+        const uint64_t cbase = readlane64(tbv, 0), cend = readlane64(tbv, 1);
+        const bool skip = cend > n || cbase >= cend;  // empty, or malformed (flagged by rl_offsets_kernel)
         s_val4[tid] = vv;
         const u32x4 vv_cur = vv;
         uint32_t c[RPT];
@@ -1008,8 +1056,7 @@ __global__ __launch_bounds__(kRdThreads) void rl_decode_kernel(
         if (next < ntiles) {  // next tile's loads in flight during this one
             cv = load16_tail(counts, next * kRdRuns + tid * RPT, runs);
             vv = load16_tail(values, next * kRdRuns + tid * RPT, runs);
-            base = tile_base[next];
-            end = tile_base[next + 1];
+            tbv = tile_base[next + (lane & 1)];
         }
         if (!skip) {
             const uint32_t inc = wave_incl_scan_u32(sum);
@@ -1195,6 +1242,271 @@ __global__ __launch_bounds__(kRdThreads) void rl_decode_kernel(
 }
 
 
+// ---- decode, one wave per tile of 64 x RPL runs (dense inputs) -----------
+// The block decode above spends its time on per-tile overhead when runs are
+// short (a 4096-run tile of random bytes is only 4 KiB of output: three block
+// barriers and a byte-memset loop that the compiler turns into ~30
+// instructions per run). Here every wave decodes its own tiles (grid-stride
+// over waves) with no block barrier: lane l holds runs RPL l .. RPL l + RPL - 1
+// (RPL/16 count and value vectors), a wave scan places them, and the output is
+// built by the same rank method per 8 KiB window -- each run's start bit is
+// ds_or'ed into a wave-private bitmap (lane-contiguous runs: one instruction's
+// targets are a lane's output length apart, <= 2 lanes per word for 1-byte
+// runs), a wave scan of the words' popcounts ranks every 16-byte chunk, and
+// each lane assembles whole chunks by byte permutes over the 16 values from the
+// chunk's first run on and stores them coalesced. The two chunks a tile shares
+// with its neighbours are stored as aligned 1/2/4/8-byte pieces. The offsets
+// pre-pass runs at the wave tile's granularity for this kernel.
+#ifndef FLRL_RL_WD_RPL
+#define FLRL_RL_WD_RPL 32
+#endif
+constexpr int kWdRpl = FLRL_RL_WD_RPL;     // runs per lane
+constexpr int kWdRuns = kWave * kWdRpl;    // runs per wave tile
+constexpr int kWdWin = 8192;               // output bytes per window
+constexpr int kWdWords = kWdWin / 32;      // bitmap words per window (4 per lane)
+constexpr int kWdThreads = 256;
+#ifndef FLRL_RL_WD_PER_CU
+#define FLRL_RL_WD_PER_CU (FLRL_RL_WD_RPL == 16 ? 8 : 6)
+#endif
+constexpr int kWdPerCU = FLRL_RL_WD_PER_CU;  // resident workgroups per CU
+// inputs with a mean run of at most this many bytes take the wave decode
+#ifndef FLRL_RL_DENSE_MEAN
+#define FLRL_RL_DENSE_MEAN 24
+#endif
+constexpr uint64_t kWdDenseMean = FLRL_RL_DENSE_MEAN;
+static_assert(kWdWords == 4 * kWave, "one bitmap vector per lane");
+static_assert(kWdRpl % 16 == 0, "whole vectors per lane");
+
+__device__ __forceinline__ void wave_lds_sync()
+{
+    // LDS operations of one wave complete in order; the fences keep the
+    // compiler from moving LDS accesses across this point
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Bytes [lo, hi) of the 16-byte chunk v (0 <= lo < hi <= 16) stored at dst (16-byte
+// aligned) as naturally aligned pieces: 1, 2, 4, 8 bytes up to a 16-byte
+// boundary, then 8, 4, 2, 1 while they fit.
+__device__ __forceinline__ void store_chunk_part(uint8_t *dst, u32x4 v, uint32_t lo, uint32_t hi)
+{
+    auto dw = [&](uint32_t a) { return a < 8 ? (a < 4 ? v[0] : v[1]) : (a < 12 ? v[2] : v[3]); };
+    auto qw = [&](uint32_t a) {
+        return a < 8 ? ((uint64_t)v[1] << 32) | v[0] : ((uint64_t)v[3] << 32) | v[2];
+    };
+    uint32_t a = lo;
+    if ((a & 1u) && a + 1 <= hi) {
+        dst[a] = (uint8_t)(dw(a) >> (8 * (a & 3)));
+        a += 1;
+    }
+    if ((a & 2u) && a + 2 <= hi) {
+        *reinterpret_cast<uint16_t *>(dst + a) = (uint16_t)(dw(a) >> (8 * (a & 3)));
+        a += 2;
+    }
+    if ((a & 4u) && a + 4 <= hi) {
+        *reinterpret_cast<uint32_t *>(dst + a) = dw(a);
+        a += 4;
+    }
+    if ((a & 8u) && a + 8 <= hi) {
+        *reinterpret_cast<uint64_t *>(dst + a) = qw(a);
+        a += 8;
+    }
+    if (a + 8 <= hi) {
+        *reinterpret_cast<uint64_t *>(dst + a) = qw(a);
+        a += 8;
+    }
+    if (a + 4 <= hi) {
+        *reinterpret_cast<uint32_t *>(dst + a) = dw(a);
+        a += 4;
+    }
+    if (a + 2 <= hi) {
+        *reinterpret_cast<uint16_t *>(dst + a) = (uint16_t)(dw(a) >> (8 * (a & 3)));
+        a += 2;
+    }
+    if (a + 1 <= hi)
+        dst[a] = (uint8_t)(dw(a) >> (8 * (a & 3)));
+}
+
+__global__ __launch_bounds__(kWdThreads) void rl_decode_wave_kernel(
+    const uint8_t *__restrict__ counts, const uint8_t *__restrict__ values, uint64_t runs,
+    uint8_t *__restrict__ out, uint64_t n, const uint64_t *__restrict__ tile_base, uint64_t ntiles)
+{
+    constexpr int NW = kWdThreads / kWave;
+    constexpr int NV = kWdRpl / 16;  // count / value vectors per lane
+    __shared__ u32x4 s_val4[NW][kWdRuns / 16 + 2];  // +32 B: the permute window reads up to 19 bytes past a run
+    __shared__ u32x4 s_bm4[NW][kWdWords / 4 + 1];   // +1: a single-window tile's past-the-end marks
+    __shared__ u32x4 s_pre4[NW][kWdWords / 4];      // starts in the window before word w
+    __shared__ uint64_t s_pfx[256];                 // byte i of s_pfx[x] = popcount(x & ((2 << i) - 1))
+    const int tid = threadIdx.x;
+    const int lane = tid & (kWave - 1);
+    const int wave = tid / kWave;
+    {
+        static_assert(kWdThreads == 256, "one table entry per thread");
+        uint64_t e = 0;
+        uint32_t c = 0;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            c += (tid >> i) & 1;
+            e |= (uint64_t)c << (8 * i);
+        }
+        s_pfx[tid] = e;
+    }
+    __syncthreads();  // the only block barrier
+    const uint64_t stride = (uint64_t)gridDim.x * NW;
+    uint64_t tile = (uint64_t)blockIdx.x * NW + wave;
+    if (tile >= ntiles)
+        return;
+    u32x4 *const sv4 = s_val4[wave];
+    const uint32_t *const sv32 = reinterpret_cast<const uint32_t *>(sv4);
+    u32x4 *const bm4 = s_bm4[wave];
+    uint32_t *const bm = reinterpret_cast<uint32_t *>(bm4);
+    u32x4 *const pre4 = s_pre4[wave];
+    const uint32_t *const pre = reinterpret_cast<const uint32_t *>(pre4);
+    if (lane < 2)
+        sv4[kWdRuns / 16 + lane] = u32x4{0u, 0u, 0u, 0u};
+    u32x4 cv[NV], vv[NV];
+    // a tile's count and value vectors (zeros past the last run)
+    auto load_tile = [&](uint64_t t) {
+        const uint64_t r = t * kWdRuns + lane * kWdRpl;
+        if ((t + 1) * kWdRuns <= runs) {  // uniform: no per-load tail checks
+#pragma unroll
+            for (int v = 0; v < NV; ++v) {
+                cv[v] = *reinterpret_cast<const u32x4 *>(counts + r + 16 * v);
+                vv[v] = *reinterpret_cast<const u32x4 *>(values + r + 16 * v);
+            }
+        } else {  // the last tile: counts are masked when used
+#pragma unroll
+            for (int v = 0; v < NV; ++v) {
+                cv[v] = load16_clamped(counts, r + 16 * v, runs);
+                vv[v] = load16_clamped(values, r + 16 * v, runs);
+            }
+        }
+    };
+    load_tile(tile);
+    uint64_t tbv = tile_base[tile + (lane & 1)];  // vector load: lane 0 start, lane 1 end
+    for (;;) {
+        const uint64_t next = tile + stride;
+        const uint64_t base = readlane64(tbv, 0), end = readlane64(tbv, 1);
+        wave_lds_sync();  // the previous tile's readers of the values are done
+        u32x4 cc[NV];     // counts stay packed
+        uint32_t S = 0;
+        const bool last = (tile + 1) * kWdRuns > runs;
+#pragma unroll
+        for (int v = 0; v < NV; ++v) {
+            sv4[lane * NV + v] = vv[v];
+            cc[v] = cv[v];
+            if (last) {  // zero counts past the last run
+                const uint32_t valid = valid16(tile * kWdRuns + lane * kWdRpl + 16 * v, runs);
+#pragma unroll
+                for (int d = 0; d < 4; ++d)
+                    cc[v][d] = mask_dword(cc[v][d], valid, d);
+            }
+#pragma unroll
+            for (int d = 0; d < 4; ++d)
+                S = __builtin_amdgcn_udot4(cc[v][d], 0x01010101u, S, false);
+        }
+        if (next < ntiles) {  // next tile's loads in flight during this one
+            load_tile(next);
+            tbv = tile_base[next + (lane & 1)];
+        }
+        if (end <= n && base < end) {  // else empty, or malformed (flagged by rl_offsets_kernel)
+            const uint32_t inc = wave_incl_scan_u32(S);
+            const uint64_t g0 = base & ~15ull;
+            const uint32_t o = (uint32_t)(base - g0) + inc - S;  // window-relative start of the lane's first run
+            const uint32_t len = (uint32_t)(end - g0);
+            uint32_t starts_before = 0;  // runs starting before the window
+            for (uint32_t w = 0; w < len; w += kWdWin) {
+                bm4[lane] = u32x4{0u, 0u, 0u, 0u};
+                wave_lds_sync();
+                // (1) start bits of this lane's runs that begin in [w, w + W)
+                uint32_t p = o - w;
+                if (len <= (uint32_t)kWdWin) {
+                    // one window: every start is in it; a zero count (past the last run)
+                    // marks the lane's end, which is the next start or the tile's end
+#pragma unroll
+                    for (int i = 0; i < kWdRpl; ++i) {
+                        atomicOr(&bm[p >> 5], 1u << (p & 31));
+                        p += (cc[i >> 4][(i >> 2) & 3] >> (8 * (i & 3))) & 0xFFu;
+                    }
+                } else {
+#pragma unroll
+                    for (int i = 0; i < kWdRpl; ++i) {
+                        const uint32_t ci = (cc[i >> 4][(i >> 2) & 3] >> (8 * (i & 3))) & 0xFFu;
+                        if (ci != 0 && p < (uint32_t)kWdWin)
+                            atomicOr(&bm[p >> 5], 1u << (p & 31));
+                        p += ci;
+                    }
+                }
+                wave_lds_sync();
+                // (2) popcount prefix over the window's words; lane owns words 4 lane .. 4 lane + 3
+                const u32x4 wd = bm4[lane];
+                const uint32_t p0 = __popc(wd[0]), p1 = __popc(wd[1]), p2 = __popc(wd[2]), p3 = __popc(wd[3]);
+                const uint32_t tsum = p0 + p1 + p2 + p3;
+                const uint32_t tinc = wave_incl_scan_u32(tsum);
+                const uint32_t e0 = tinc - tsum;
+                pre4[lane] = u32x4{e0, e0 + p0, e0 + p0 + p1, e0 + p0 + p1 + p2};
+                const uint32_t wtot = (uint32_t)__builtin_amdgcn_readlane((int)tinc, kWave - 1);
+                wave_lds_sync();
+                // (3) chunks q = lane + 64 k of the window
+                const uint32_t wl = len - w < (uint32_t)kWdWin ? len - w : (uint32_t)kWdWin;
+                const uint32_t nch = (wl + 15) / 16;
+                for (uint32_t q = lane; q < nch; q += kWave) {
+                    const uint32_t gq = w + 16u * q;  // window-relative chunk start
+                    const uint32_t word = bm[q >> 1];
+                    const uint32_t m = (q & 1) ? word >> 16 : word & 0xFFFFu;
+                    const uint32_t pq = pre[q >> 1] + ((q & 1) ? __popc(word & 0xFFFFu) : 0u);
+                    int32_t r = (int32_t)(starts_before + pq + (m & 1u)) - 1;  // run of byte 0
+                    uint32_t m1 = m & 0xFFFEu;  // starts after byte 0
+                    if (r < 0) {  // bytes before the tile's first start are not stored
+                        m1 &= m1 - 1;
+                        r = 0;
+                    }
+                    u32x4 ov;
+                    if (m1 == 0) {
+                        const uint32_t s4 = __builtin_amdgcn_perm(0u, reinterpret_cast<const uint8_t *>(sv32)[r], 0u);
+                        ov = u32x4{s4, s4, s4, s4};
+                    } else {
+                        // byte i takes run r + k_i, k_i = starts in bytes 1..i (<= 15)
+                        const uint32_t a = (uint32_t)r >> 2, sh = (uint32_t)r & 3u;
+                        const uint32_t d0 = sv32[a], d1 = sv32[a + 1], d2 = sv32[a + 2], d3 = sv32[a + 3],
+                                       d4 = sv32[a + 4];
+                        const uint32_t w0 = __builtin_amdgcn_alignbyte(d1, d0, sh);
+                        const uint32_t w1 = __builtin_amdgcn_alignbyte(d2, d1, sh);
+                        const uint32_t w2 = __builtin_amdgcn_alignbyte(d3, d2, sh);
+                        const uint32_t w3 = __builtin_amdgcn_alignbyte(d4, d3, sh);
+                        // (no multiplies: v_mul_lo_u32 is a quarter-rate instruction)
+                        const uint64_t klo = s_pfx[m1 & 0xFFu], kh = s_pfx[m1 >> 8];
+                        const uint32_t plo = __builtin_amdgcn_perm(0u, (uint32_t)__popc(m1 & 0xFFu), 0u);
+                        const uint32_t k4[4] = {(uint32_t)klo, (uint32_t)(klo >> 32), (uint32_t)kh + plo,
+                                                (uint32_t)(kh >> 32) + plo};
+#pragma unroll
+                        for (int d = 0; d < 4; ++d) {
+                            const uint32_t sel = k4[d];
+                            const uint32_t lo8 = __builtin_amdgcn_perm(w1, w0, sel & 0x07070707u);
+                            const uint32_t hi8 = __builtin_amdgcn_perm(w3, w2, sel & 0x07070707u);
+                            // byte i from hi8 (selector 4 + i) where k_i >= 8, else from lo8 (i)
+                            ov[d] = __builtin_amdgcn_perm(hi8, lo8, ((sel >> 1) & 0x04040404u) | 0x03020100u);
+                        }
+                    }
+                    const uint32_t b0 = (uint32_t)(base - g0);
+                    const uint32_t lo = gq < b0 ? b0 - gq : 0u;
+                    const uint32_t hi = gq + 16 > len ? len - gq : 16u;
+                    if (lo == 0 && hi == 16)
+                        *reinterpret_cast<u32x4 *>(out + g0 + gq) = ov;  // plain stores, as the block decode
+                    else  // a chunk shared with a neighbouring tile: its bytes only
+                        store_chunk_part(out + g0 + gq, ov, lo, hi);
+                }
+                starts_before += wtot;
+                wave_lds_sync();  // chunk readers of the bitmap are done before it is cleared
+            }
+        }
+        if (next >= ntiles)
+            break;
+        tile = next;
+    }
+}
+
 struct RlEncLayout {
     size_t tiles, zero, bytes;
     explicit RlEncLayout(size_t n)
@@ -1207,15 +1519,21 @@ struct RlEncLayout {
 
 struct RlDecLayout {
     size_t tiles, blocks, iters, zero, bytes;
-    explicit RlDecLayout(size_t runs)
+    // tile_base is sized for the finer (wave) tiles; `tiles` counts the tiles
+    // of the decode chosen for (runs, n)
+    explicit RlDecLayout(size_t runs, size_t n = 0)
     {
-        tiles = div_up(runs, (size_t)kRdRuns);
+        const bool dense = n != 0 && n <= kWdDenseMean * runs;
+        tiles = div_up(runs, (size_t)(dense ? kWdRuns : kRdRuns));
         // offsets rounds per workgroup: the grid stays within kMaxPrefixBlocks
         iters = div_up(div_up(runs, (size_t)kRoRuns), (size_t)kMaxPrefixBlocks);
         iters = iters ? iters : 1;
         blocks = div_up(runs, (size_t)kRoRuns * iters);
         zero = sizeof(Ctrl) + round_up(blocks * 8, 16);
-        bytes = zero + round_up((tiles + 1) * 8, 16);
+        // the size a caller allocates must not shrink as runs grow (callers size
+        // scratch for an upper bound of runs): bound blocks monotonically
+        const size_t bmax = std::min(div_up(runs, (size_t)kRoRuns), (size_t)kMaxPrefixBlocks);
+        bytes = sizeof(Ctrl) + round_up(bmax * 8, 16) + round_up((div_up(runs, (size_t)kWdRuns) + 1) * 8, 16);
     }
 };
 
@@ -1266,7 +1584,8 @@ extern "C" int flrl_rl_decode_device(const uint8_t *d_counts, const uint8_t *d_v
                                      size_t scratch_bytes, void *stream)
 {
     hipStream_t s = static_cast<hipStream_t>(stream);
-    const RlDecLayout L(runs);
+    const RlDecLayout L(runs, n);
+    const bool dense = n != 0 && n <= kWdDenseMean * runs;
     if (!d_scratch)
         return set_error(FLRL_E_ARG, "flrl_rl_decode_device: null scratch");
     if (scratch_bytes < L.bytes)
@@ -1294,7 +1613,23 @@ extern "C" int flrl_rl_decode_device(const uint8_t *d_counts, const uint8_t *d_v
     uint64_t *status = reinterpret_cast<uint64_t *>(ctrl + 1);
     uint64_t *tile_base =
         reinterpret_cast<uint64_t *>(static_cast<uint8_t *>(d_scratch) + L.zero);
-    hipLaunchKernelGGL(rl_offsets_kernel, dim3((uint32_t)L.blocks), dim3(kThreads), 0, s, d_counts,
+    if (dense) {
+        // mean run <= kWdDenseMean bytes: 1024-run tiles, one wave each
+        hipLaunchKernelGGL(rl_offsets_kernel<kWdRuns>, dim3((uint32_t)L.blocks), dim3(kRoThreads), 0, s, d_counts,
+                           (uint64_t)runs, (uint64_t)n, tile_base, (uint32_t)L.tiles,
+                           (uint32_t)L.blocks, (uint32_t)L.iters, ctrl, status);
+        FLRL_HIP(hipGetLastError());
+        const size_t wgs = div_up(L.tiles, (size_t)(kWdThreads / kWave));
+        const size_t wgrid = (size_t)kWdPerCU * (size_t)cu_count();
+        kernel_timing_begin(s);
+        hipLaunchKernelGGL(rl_decode_wave_kernel, dim3((uint32_t)(wgs < wgrid ? wgs : wgrid)), dim3(kWdThreads),
+                           0, s, d_counts, d_values, (uint64_t)runs, d_out, (uint64_t)n, tile_base,
+                           (uint64_t)L.tiles);
+        kernel_timing_end(s);
+        FLRL_HIP(hipGetLastError());
+        return FLRL_OK;
+    }
+    hipLaunchKernelGGL(rl_offsets_kernel<kRdRuns>, dim3((uint32_t)L.blocks), dim3(kRoThreads), 0, s, d_counts,
                        (uint64_t)runs, (uint64_t)n, tile_base, (uint32_t)L.tiles,
                        (uint32_t)L.blocks, (uint32_t)L.iters, ctrl, status);
     FLRL_HIP(hipGetLastError());

@@ -84,3 +84,14 @@ def test_time_next_kernel_arguments():
     assert f(None, None) == flrl.E_OK
     with pytest.raises(ValueError):
         flrl.time_next_kernel(0, 0)  # a not-yet-created event handle
+
+
+def test_scratch_sizes_monotone():
+    # callers size scratch once for an upper bound (RLDevice: runs <= n; the
+    # streamed decode: runs <= chunk), so a smaller count must never need more
+    k = 32768 * 1024  # decode pre-pass: one more round per workgroup past this many runs
+    pts = sorted({1, 2, 2047, 2048, 2049, 4096, 32767, 32768, 32769, 10 ** 6}
+                 | {m * k + d for m in (1, 2, 3, 7) for d in (-32769, -1, 0, 1, 32768, 10 ** 6)})
+    for f in (flrl.rl_decode_scratch_bytes, flrl.rl_scratch_bytes, flrl.fl_scratch_bytes):
+        sizes = [f(x) for x in pts]
+        assert sizes == sorted(sizes), f.__name__

@@ -192,6 +192,38 @@ def test_decode_all_starts_in_chunk():
     check(a)
 
 
+# ---- wave decode (mean run <= 24 bytes: one wave per 2048-run tile) --------
+@pytest.mark.parametrize("runlen", [23, 24, 25])
+def test_decode_wave_threshold(runlen):
+    # mean run exactly at, below and above the wave-decode threshold
+    nruns = 5 * 2048 + 31
+    vals = (np.arange(nruns) * 29 % 253 + 1).astype(np.uint8)
+    check(np.repeat(vals, runlen))
+
+
+@pytest.mark.parametrize("seed", [4, 5, 6])
+def test_decode_wave_long_runs_in_dense(seed):
+    # mostly 1-byte runs with a few runs of 100..255 bytes: a dense input (wave
+    # decode) whose tiles have one to six 8 KiB output windows
+    rng = np.random.default_rng(seed)
+    lens = np.where(rng.random(300_000) < 0.08, rng.integers(100, 256, 300_000), 1)
+    vals = (np.cumsum(rng.integers(1, 255, size=lens.size)) % 256).astype(np.uint8)
+    a = np.repeat(vals, lens)
+    assert a.size <= 24 * lens.size
+    check(a)
+
+
+def test_decode_wave_rejects_zero_count():
+    # a zero count inside a dense input (and inside the last, partial tile)
+    for pos in (1000, 2048 * 3 + 5):
+        counts = np.ones(2048 * 3 + 100, np.uint8)
+        counts[pos] = 0
+        values = (np.arange(counts.size) % 250).astype(np.uint8)
+        with pytest.raises(flrl.FLRLError) as e:
+            flrl.rl_decompress(int(counts.sum()), counts, values)
+        assert e.value.code == flrl.E_FORMAT
+
+
 def test_device_more_than_2_32_runs():
     """64-bit run indices: ~4.27 GiB of random bytes has R > 2^32 runs (all
     shorter than 255). Device round trip; R against an independent torch count
