@@ -9,7 +9,7 @@ OP=$1; KIND=$2; LIB=${3:-fl-rl-compression-mpi_amd/lib/libflrl.so}; TAG=${4:-$OP
 OUT=gpurun_out/pmc_ab/$TAG
 rm -rf "$OUT"; mkdir -p "$OUT"
 CMD=(python3 scripts/ab_libs.py --op "$OP" --libs "$LIB" --kind "$KIND" --reps 4)
-timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- "${CMD[@]}" > "$OUT/trace.log" 2>&1 || { echo "trace failed"; tail -5 "$OUT/trace.log"; exit 1; }
+timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- "${CMD[@]}" > "$OUT/trace.log" 2>&1 || [ -n "$ALLOWFAIL" ] || { echo "trace failed"; tail -5 "$OUT/trace.log"; exit 1; }
 [ -n "$NOPMC" ] && { python3 scripts/pmc_summary.py "$OUT"; exit 0; }
 i=0
 for grp in "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVES SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD" \
