@@ -1420,22 +1420,22 @@ __global__ __launch_bounds__(kWdThreads) void rl_decode_wave_kernel(
                 bm4[lane] = u32x4{0u, 0u, 0u, 0u};
                 wave_lds_sync();
                 // (1) start bits of this lane's runs that begin in [w, w + W)
+                // A zero count (past the last run; or malformed, flagged by the pre-pass)
+                // marks the position of the next start or the tile's end again: harmless
+                // (the bitmap has a word past the window for the latter).
                 uint32_t p = o - w;
-                if (len <= (uint32_t)kWdWin) {
-                    // one window: every start is in it; a zero count (past the last run)
-                    // marks the lane's end, which is the next start or the tile's end
+                if (len <= (uint32_t)kWdWin) {  // one window: every start is in it
 #pragma unroll
                     for (int i = 0; i < kWdRpl; ++i) {
-                        atomicOr(&bm[p >> 5], 1u << (p & 31));
+                        atomicOr(bm + __builtin_amdgcn_ubfe(p, 5, 27), 1u << (p & 31));
                         p += (cc[i >> 4][(i >> 2) & 3] >> (8 * (i & 3))) & 0xFFu;
                     }
                 } else {
 #pragma unroll
                     for (int i = 0; i < kWdRpl; ++i) {
-                        const uint32_t ci = (cc[i >> 4][(i >> 2) & 3] >> (8 * (i & 3))) & 0xFFu;
-                        if (ci != 0 && p < (uint32_t)kWdWin)
-                            atomicOr(&bm[p >> 5], 1u << (p & 31));
-                        p += ci;
+                        if (p <= (uint32_t)kWdWin)
+                            atomicOr(bm + __builtin_amdgcn_ubfe(p, 5, 27), 1u << (p & 31));
+                        p += (cc[i >> 4][(i >> 2) & 3] >> (8 * (i & 3))) & 0xFFu;
                     }
                 }
                 wave_lds_sync();
