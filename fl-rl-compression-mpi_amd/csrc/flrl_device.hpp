@@ -118,6 +118,13 @@ __device__ __forceinline__ uint32_t dpp_up0(uint32_t v)
     return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, RM, 0xF, true);
 }
 
+// The value of lane i-1 (lane 0: 0), by DPP wave_shr:1 instead of an LDS
+// crossbar round trip (ds_bpermute).
+__device__ __forceinline__ uint32_t wave_shr1(uint32_t v)
+{
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xF, 0xF, false);
+}
+
 // Inclusive wave scan in six DPP steps (no LDS crossbar round trips):
 // row_shr 1/2/4/8 scan each row, row_bcast:15 and :31 carry row totals up.
 __device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t v)

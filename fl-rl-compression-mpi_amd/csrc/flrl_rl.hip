@@ -90,27 +90,24 @@ constexpr int kRdRuns = 4096;        // runs per decode tile
 constexpr int kRdThreads = 256;
 constexpr int kRdPerCU = 4;          // resident decode workgroups per CU (LDS 37 KB each)
 
-// ---- PhaseMap packed in a u32: bit 8 = constant, bits 0-7 = value (< 255) ----
+// ---- PhaseMap packed in a u32: bit 31 = constant, bits 0-30 = value --------
+// The value is kept unreduced (a byte count within one tile, < 2^31) and taken
+// mod 255 only when the map is applied, so composing is one add and a select
+// (the reduced form needed a compare, a subtract and two masks per step).
 constexpr uint32_t kMapIdent = 0;
+constexpr uint32_t kMapConst = 0x80000000u;
 __device__ __forceinline__ uint32_t pm_make(bool constant, uint32_t v)
 {
-    return (constant ? 0x100u : 0u) | v;
+    return (constant ? kMapConst : 0u) | v;
 }
 // a then b
 __device__ __forceinline__ uint32_t pm_compose(uint32_t a, uint32_t b)
 {
-    if (b & 0x100u)
-        return b;
-    uint32_t v = (a & 0xFFu) + (b & 0xFFu);
-    v = v >= 255u ? v - 255u : v;
-    return (a & 0x100u) | v;
+    return (b & kMapConst) ? b : a + b;
 }
 __device__ __forceinline__ uint32_t pm_apply(uint32_t m, uint32_t c)
 {
-    if (m & 0x100u)
-        return m & 0xFFu;
-    const uint32_t v = c + (m & 0xFFu);
-    return v >= 255u ? v - 255u : v;
+    return ((m & kMapConst) ? (m & ~kMapConst) : c + m) % 255u;
 }
 // inclusive PhaseMap scan, DPP steps as wave_incl_scan_u32 (0 = identity map)
 __device__ __forceinline__ uint32_t wave_incl_scan_map(uint32_t m)
@@ -367,7 +364,7 @@ struct RlWave {
         uint32_t rel_st;  // PhaseMap over the staged sub-chunks
         uint32_t v0;      // the chunk's first byte
         __device__ uint32_t pre() const { return first != kNone ? first : len; }
-        __device__ uint64_t map() const { return first != kNone ? sm_nat(first, K, rel_in & 0xFFu) : sm_nonat(len); }
+        __device__ uint64_t map() const { return first != kNone ? sm_nat(first, K, pm_apply(rel_in, 0)) : sm_nonat(len); }
     };
 
     const uint8_t *in;
@@ -450,7 +447,7 @@ struct RlWave {
             L.sfirst = acc & 1u ? 0u : kNone;
             return mylast;
         }
-        const uint32_t up = (uint32_t)__shfl_up((int)mylast, 1, kWave);
+        const uint32_t up = wave_shr1(mylast);
         L.p0 = lane == 0 ? p_sub : up;
         {
             uint32_t p = L.p0;
@@ -481,12 +478,12 @@ struct RlWave {
         const bool has = L.ncnt != 0;
         const uint32_t lmap = has ? pm_make(true, L.vbl - L.lpos) : pm_make(false, L.vbl);
         const uint32_t incl = wave_incl_scan_map(lmap);
-        uint32_t lexcl = __shfl_up(incl, 1, kWave);
+        uint32_t lexcl = wave_shr1(incl);
         L.lrel = lane == 0 ? kMapIdent : lexcl;
         L.smap = (uint32_t)__builtin_amdgcn_readlane((int)incl, kWave - 1);
         const unsigned long long hb = __ballot(has);
         const int fl = hb ? __ffsll(hb) - 1 : 0;
-        const uint32_t ff = (uint32_t)__shfl(L.fpos, fl, kWave);
+        const uint32_t ff = (uint32_t)__builtin_amdgcn_readlane((int)L.fpos, fl);  // fl is uniform
         L.sfirst = hb ? (uint32_t)fl * LB + ff : kNone;
         return (uint32_t)__builtin_amdgcn_readlane((int)mylast, kWave - 1);
     }
@@ -768,8 +765,11 @@ struct RlWave {
 // One tile per workgroup (grid = tiles), in ticket order: stage, publish the
 // tile map, ONE look-back by wave 0 while waves 1-3 wait, emit. Three block
 // barriers per tile (ticket, wave maps, state).
+#ifndef FLRL_RL_MINW
+#define FLRL_RL_MINW 1
+#endif
 template <int T, int LB, int SUB>
-__global__ __launch_bounds__(T) void rl_encode_wave_kernel(
+__global__ __launch_bounds__(T, FLRL_RL_MINW) void rl_encode_wave_kernel(
     const uint8_t *__restrict__ in, uint64_t n, uint32_t ntiles, uint8_t *__restrict__ counts,
     uint8_t *__restrict__ values, uint64_t *__restrict__ runs_out, Ctrl *ctrl, uint64_t *status)
 {
