@@ -94,6 +94,8 @@ def parse():
                    help="PMC summary (scripts/summarize_profile.py); default profiles/traffic_<kind>_<bytes>.json")
     p.add_argument("--no-north-star", action="store_true",
                    help="skip the 16 GiB-per-GPU u8 FL encode (north star at N=1, configs[4] at N>1)")
+    p.add_argument("--no-rl-dense", action="store_true",
+                   help="skip the random-bytes RL section (profiles average kernels per name)")
     p.add_argument("--no-rl", action="store_true",
                    help="skip the RL section (config #3: 1 GiB runs32), which runs at N=1 only")
     p.add_argument("--force-scan", action="store_true",
@@ -266,11 +268,9 @@ def north_star_section(seed: int, steps: int, warmup: int, dev):
     return res
 
 
-def rl_section(n: int, seed: int, steps: int, warmup: int, dev, cpu: bool):
-    """BASELINE configs[2]: RL encode/decode of n bytes of runs32 (mean run 32).
-    Input generated on the host by the product generator (runs32 is
-    sequential), copied to HBM before timing."""
-    x = torch.from_numpy(flrl.gen_host("runs32", n, seed)).to(dev)
+def _rl_timed(x, n: int, steps: int, warmup: int, dev):
+    """RL encode + decode of x (n bytes in HBM): R, the round trip, and mean
+    whole-call / kernel-alone times of both (HIP events)."""
     d = RLDevice(n, dev)
     stream = torch.cuda.current_stream()
     d.encode(x)
@@ -293,8 +293,36 @@ def rl_section(n: int, seed: int, steps: int, warmup: int, dev, cpu: bool):
     torch.cuda.synchronize()
     if d.error():
         raise SystemExit(f"RL device error {d.error()} during the timed steps")
-    enc_ms, dec_ms = mean_ms(ev, 0, 1), mean_ms(ev, 1, 2)  # whole calls
-    enc_k, dec_k = mean_ms(ev, 3, 4), mean_ms(ev, 5, 6)      # kernels alone
+    t = (mean_ms(ev, 0, 1), mean_ms(ev, 1, 2), mean_ms(ev, 3, 4), mean_ms(ev, 5, 6))
+    return d, R, ok, t
+
+
+def rl_dense_section(n: int, seed: int, steps: int, warmup: int, dev):
+    """RL of n uniform-random bytes (mean run 1.004: the densest input; decode
+    takes the wave-tile kernel): kernel and call times, device round trip."""
+    from flrl.device import gen
+    x = gen("u8", n, seed)
+    d, R, ok, (enc_ms, dec_ms, enc_k, dec_k) = _rl_timed(x, n, steps, warmup, dev)
+    alg = n + 2 * R
+    res = {"workload": f"RL encode+decode of {n} uniform-random bytes (u8, seed {seed})", "runs": R,
+           "rl_encode": {"ms": round(enc_k, 4), "call_ms": round(enc_ms, 4),
+                         "alg_GBps": round(alg / (enc_k * 1e-3) / 1e9, 1)},
+           "rl_decode": {"ms": round(dec_k, 4), "call_ms": round(dec_ms, 4),
+                         "alg_GBps": round(alg / (dec_k * 1e-3) / 1e9, 1),
+                         "call_alg_GBps": round(alg / (dec_ms * 1e-3) / 1e9, 1)},
+           "roundtrip": ok}
+    del x, d
+    torch.cuda.empty_cache()
+    return res
+
+
+def rl_section(n: int, seed: int, steps: int, warmup: int, dev, cpu: bool):
+    """BASELINE configs[2]: RL encode/decode of n bytes of runs32 (mean run 32).
+    Input generated on the host by the product generator (runs32 is
+    sequential), copied to HBM before timing."""
+    x = torch.from_numpy(flrl.gen_host("runs32", n, seed)).to(dev)
+    d, R, ok, (enc_ms, dec_ms, enc_k, dec_k) = _rl_timed(x, n, steps, warmup, dev)
+    out = d.out[:n]
     alg = n + 2 * R  # SURVEY.md §8(d): RL encode N+2R, decode 2R+N
     res = {
         "workload": f"RL encode+decode of {n} bytes runs32 (seed {seed}), BASELINE configs[2]",
@@ -306,7 +334,8 @@ def rl_section(n: int, seed: int, steps: int, warmup: int, dev, cpu: bool):
                       "frac": round(alg / (enc_k * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
         "rl_decode": {"ms": round(dec_k, 4), "call_ms": round(dec_ms, 4),
                       "alg_GBps": round(alg / (dec_k * 1e-3) / 1e9, 1),
-                      "frac": round(alg / (dec_k * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
+                      "frac": round(alg / (dec_k * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                      "call_frac": round(alg / (dec_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
         "roundtrip": ok,
     }
     if cpu:
@@ -572,6 +601,8 @@ def main():
         rl = None
         if world == 1 and not args.no_rl:
             rl = rl_section(n, args.seed, args.steps, args.warmup, dev, cpu=sample > 0)
+            if not args.no_rl_dense:
+                rl["dense_u8"] = rl_dense_section(n, args.seed, args.steps, args.warmup, dev)
         line = {
             "metric": METRIC,
             "value": round(value, 2),
