@@ -56,7 +56,7 @@ constexpr int kDecItems = 8;      // decode tile = 512 lanes x 8 x 16 B = 64 KiB
 constexpr int kDecPerCU = 2;      // persistent decode workgroups per CU (LDS 64 KiB each)
 constexpr int kDecTileBytes = kDecThreads * 16 * kDecItems;
 constexpr int kDecTileFrames = kDecTileBytes / kFrame;
-constexpr int kOffFramesPerThread = 64;
+constexpr int kOffFramesPerThread = 128;  // (64: 1 GiB decode call +1 %, more workgroups to scan; 256: equal)
 constexpr int kOffFrames = kThreads * kOffFramesPerThread;  // frames per offsets workgroup
 constexpr int kOffLanesPerTile = kDecTileFrames / kOffFramesPerThread;  // offsets lanes per decode tile
 static_assert(kOffLanesPerTile * kOffFramesPerThread == kDecTileFrames && kThreads % kOffLanesPerTile == 0,
