@@ -848,6 +848,11 @@ constexpr int kRoWaves = kRoThreads / kWave;
 constexpr int kRoQ = 16;                                // count vectors per lane per step
 constexpr int kRoStep = kRoQ * 16 * kWave;              // counts per wave step (16384)
 constexpr int kRoRuns = kRoStep * kRoWaves;             // counts per workgroup and iteration
+#ifndef FLRL_RL_RO_MAXB
+#define FLRL_RL_RO_MAXB 256
+#endif
+constexpr size_t kRoMaxBlocks = FLRL_RL_RO_MAXB;        // workgroups: 256 (1 GiB runs32 call -2 %; 128: random bytes +13 %; 1024: the old cap)
+static_assert(kRoMaxBlocks <= kMaxPrefixBlocks, "block_prefix_all bound");
 
 __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v)
 {
@@ -1526,7 +1531,7 @@ struct RlDecLayout {
         const bool dense = n != 0 && n <= kWdDenseMean * runs;
         tiles = div_up(runs, (size_t)(dense ? kWdRuns : kRdRuns));
         // offsets rounds per workgroup: the grid stays within kMaxPrefixBlocks
-        iters = div_up(div_up(runs, (size_t)kRoRuns), (size_t)kMaxPrefixBlocks);
+        iters = div_up(div_up(runs, (size_t)kRoRuns), (size_t)kRoMaxBlocks);
         iters = iters ? iters : 1;
         blocks = div_up(runs, (size_t)kRoRuns * iters);
         zero = sizeof(Ctrl) + round_up(blocks * 8, 16);
