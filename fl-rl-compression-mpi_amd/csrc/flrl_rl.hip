@@ -1262,25 +1262,28 @@ __global__ __launch_bounds__(kRdThreads) void rl_decode_kernel(
 // chunk's first run on and stores them coalesced. The two chunks a tile shares
 // with its neighbours are stored as aligned 1/2/4/8-byte pieces. The offsets
 // pre-pass runs at the wave tile's granularity for this kernel.
-#ifndef FLRL_RL_WD_RPL
-#define FLRL_RL_WD_RPL 32
+// Runs per lane: 32 (2048-run tiles), or 64 (4096-run tiles) for inputs with
+// a mean run of at most kWd64Mean bytes (random bytes: -7 %; runs of 1..4 and
+// longer: +2..4 %, so only the densest inputs take it).
+constexpr int kWdRpl = 32;
+constexpr int kWdRuns = kWave * kWdRpl;    // runs per wave tile (the finest tile_base granularity)
+#ifndef FLRL_RL_WD64_MEAN
+#define FLRL_RL_WD64_MEAN 2
 #endif
-constexpr int kWdRpl = FLRL_RL_WD_RPL;     // runs per lane
-constexpr int kWdRuns = kWave * kWdRpl;    // runs per wave tile
+constexpr uint64_t kWd64Mean = FLRL_RL_WD64_MEAN;
 constexpr int kWdWin = 8192;               // output bytes per window
 constexpr int kWdWords = kWdWin / 32;      // bitmap words per window (4 per lane)
 constexpr int kWdThreads = 256;
-#ifndef FLRL_RL_WD_PER_CU
-#define FLRL_RL_WD_PER_CU (FLRL_RL_WD_RPL == 16 ? 8 : 6)
-#endif
-constexpr int kWdPerCU = FLRL_RL_WD_PER_CU;  // resident workgroups per CU
+// resident workgroups per CU (VGPR-bound: 6 at 32 runs per lane, 4 at 64)
+template <int RPL>
+constexpr int wd_per_cu() { return RPL == 64 ? 4 : 6; }
 // inputs with a mean run of at most this many bytes take the wave decode
 #ifndef FLRL_RL_DENSE_MEAN
 #define FLRL_RL_DENSE_MEAN 24
 #endif
 constexpr uint64_t kWdDenseMean = FLRL_RL_DENSE_MEAN;
 static_assert(kWdWords == 4 * kWave, "one bitmap vector per lane");
-static_assert(kWdRpl % 16 == 0, "whole vectors per lane");
+
 
 __device__ __forceinline__ void wave_lds_sync()
 {
@@ -1333,13 +1336,16 @@ __device__ __forceinline__ void store_chunk_part(uint8_t *dst, u32x4 v, uint32_t
         dst[a] = (uint8_t)(dw(a) >> (8 * (a & 3)));
 }
 
+template <int RPL>
 __global__ __launch_bounds__(kWdThreads) void rl_decode_wave_kernel(
     const uint8_t *__restrict__ counts, const uint8_t *__restrict__ values, uint64_t runs,
     uint8_t *__restrict__ out, uint64_t n, const uint64_t *__restrict__ tile_base, uint64_t ntiles)
 {
     constexpr int NW = kWdThreads / kWave;
-    constexpr int NV = kWdRpl / 16;  // count / value vectors per lane
-    __shared__ u32x4 s_val4[NW][kWdRuns / 16 + 2];  // +32 B: the permute window reads up to 19 bytes past a run
+    static_assert(RPL % 16 == 0, "whole vectors per lane");
+    constexpr int NV = RPL / 16;       // count / value vectors per lane
+    constexpr int TR = kWave * RPL;    // runs per wave tile
+    __shared__ u32x4 s_val4[NW][TR / 16 + 2];  // +32 B: the permute window reads up to 19 bytes past a run
     __shared__ u32x4 s_bm4[NW][kWdWords / 4 + 1];   // +1: a single-window tile's past-the-end marks
     __shared__ u32x4 s_pre4[NW][kWdWords / 4];      // starts in the window before word w
     __shared__ uint64_t s_pfx[256];                 // byte i of s_pfx[x] = popcount(x & ((2 << i) - 1))
@@ -1369,12 +1375,12 @@ __global__ __launch_bounds__(kWdThreads) void rl_decode_wave_kernel(
     u32x4 *const pre4 = s_pre4[wave];
     const uint32_t *const pre = reinterpret_cast<const uint32_t *>(pre4);
     if (lane < 2)
-        sv4[kWdRuns / 16 + lane] = u32x4{0u, 0u, 0u, 0u};
+        sv4[TR / 16 + lane] = u32x4{0u, 0u, 0u, 0u};
     u32x4 cv[NV], vv[NV];
     // a tile's count and value vectors (zeros past the last run)
     auto load_tile = [&](uint64_t t) {
-        const uint64_t r = t * kWdRuns + lane * kWdRpl;
-        if ((t + 1) * kWdRuns <= runs) {  // uniform: no per-load tail checks
+        const uint64_t r = t * TR + lane * RPL;
+        if ((t + 1) * TR <= runs) {  // uniform: no per-load tail checks
 #pragma unroll
             for (int v = 0; v < NV; ++v) {
                 cv[v] = *reinterpret_cast<const u32x4 *>(counts + r + 16 * v);  // (non-temporal: no change)
@@ -1396,13 +1402,13 @@ __global__ __launch_bounds__(kWdThreads) void rl_decode_wave_kernel(
         wave_lds_sync();  // the previous tile's readers of the values are done
         u32x4 cc[NV];     // counts stay packed
         uint32_t S = 0;
-        const bool last = (tile + 1) * kWdRuns > runs;
+        const bool last = (tile + 1) * TR > runs;
 #pragma unroll
         for (int v = 0; v < NV; ++v) {
             sv4[lane * NV + v] = vv[v];
             cc[v] = cv[v];
             if (last) {  // zero counts past the last run
-                const uint32_t valid = valid16(tile * kWdRuns + lane * kWdRpl + 16 * v, runs);
+                const uint32_t valid = valid16(tile * TR + lane * RPL + 16 * v, runs);
 #pragma unroll
                 for (int d = 0; d < 4; ++d)
                     cc[v][d] = mask_dword(cc[v][d], valid, d);
@@ -1431,13 +1437,13 @@ __global__ __launch_bounds__(kWdThreads) void rl_decode_wave_kernel(
                 uint32_t p = o - w;
                 if (len <= (uint32_t)kWdWin) {  // one window: every start is in it
 #pragma unroll
-                    for (int i = 0; i < kWdRpl; ++i) {
+                    for (int i = 0; i < RPL; ++i) {
                         atomicOr(bm + __builtin_amdgcn_ubfe(p, 5, 27), 1u << (p & 31));
                         p += (cc[i >> 4][(i >> 2) & 3] >> (8 * (i & 3))) & 0xFFu;
                     }
                 } else {
 #pragma unroll
-                    for (int i = 0; i < kWdRpl; ++i) {
+                    for (int i = 0; i < RPL; ++i) {
                         if (p <= (uint32_t)kWdWin)
                             atomicOr(bm + __builtin_amdgcn_ubfe(p, 5, 27), 1u << (p & 31));
                         p += (cc[i >> 4][(i >> 2) & 3] >> (8 * (i & 3))) & 0xFFu;
@@ -1619,17 +1625,28 @@ extern "C" int flrl_rl_decode_device(const uint8_t *d_counts, const uint8_t *d_v
     uint64_t *tile_base =
         reinterpret_cast<uint64_t *>(static_cast<uint8_t *>(d_scratch) + L.zero);
     if (dense) {
-        // mean run <= kWdDenseMean bytes: 1024-run tiles, one wave each
-        hipLaunchKernelGGL(rl_offsets_kernel<kWdRuns>, dim3((uint32_t)L.blocks), dim3(kRoThreads), 0, s, d_counts,
-                           (uint64_t)runs, (uint64_t)n, tile_base, (uint32_t)L.tiles,
-                           (uint32_t)L.blocks, (uint32_t)L.iters, ctrl, status);
+        // mean run <= kWdDenseMean bytes: one wave per tile of 64 x RPL runs
+        const bool densest = n <= kWd64Mean * runs;
+        const size_t tiles = div_up(runs, (size_t)(densest ? 4096 : kWdRuns));
+        if (densest)
+            hipLaunchKernelGGL(rl_offsets_kernel<4096>, dim3((uint32_t)L.blocks), dim3(kRoThreads), 0, s,
+                               d_counts, (uint64_t)runs, (uint64_t)n, tile_base, (uint32_t)tiles,
+                               (uint32_t)L.blocks, (uint32_t)L.iters, ctrl, status);
+        else
+            hipLaunchKernelGGL(rl_offsets_kernel<kWdRuns>, dim3((uint32_t)L.blocks), dim3(kRoThreads), 0, s,
+                               d_counts, (uint64_t)runs, (uint64_t)n, tile_base, (uint32_t)tiles,
+                               (uint32_t)L.blocks, (uint32_t)L.iters, ctrl, status);
         FLRL_HIP(hipGetLastError());
-        const size_t wgs = div_up(L.tiles, (size_t)(kWdThreads / kWave));
-        const size_t wgrid = (size_t)kWdPerCU * (size_t)cu_count();
+        const size_t wgs = div_up(tiles, (size_t)(kWdThreads / kWave));
+        const size_t wgrid = (size_t)(densest ? wd_per_cu<64>() : wd_per_cu<32>()) * (size_t)cu_count();
+        const dim3 grid((uint32_t)(wgs < wgrid ? wgs : wgrid));
         kernel_timing_begin(s);
-        hipLaunchKernelGGL(rl_decode_wave_kernel, dim3((uint32_t)(wgs < wgrid ? wgs : wgrid)), dim3(kWdThreads),
-                           0, s, d_counts, d_values, (uint64_t)runs, d_out, (uint64_t)n, tile_base,
-                           (uint64_t)L.tiles);
+        if (densest)
+            hipLaunchKernelGGL(rl_decode_wave_kernel<64>, grid, dim3(kWdThreads), 0, s, d_counts, d_values,
+                               (uint64_t)runs, d_out, (uint64_t)n, tile_base, (uint64_t)tiles);
+        else
+            hipLaunchKernelGGL(rl_decode_wave_kernel<32>, grid, dim3(kWdThreads), 0, s, d_counts, d_values,
+                               (uint64_t)runs, d_out, (uint64_t)n, tile_base, (uint64_t)tiles);
         kernel_timing_end(s);
         FLRL_HIP(hipGetLastError());
         return FLRL_OK;

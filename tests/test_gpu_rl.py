@@ -193,7 +193,7 @@ def test_decode_all_starts_in_chunk():
 
 
 # ---- wave decode (mean run <= 24 bytes: one wave per 2048-run tile) --------
-@pytest.mark.parametrize("runlen", [23, 24, 25])
+@pytest.mark.parametrize("runlen", [1, 2, 3, 23, 24, 25])
 def test_decode_wave_threshold(runlen):
     # mean run exactly at, below and above the wave-decode threshold
     nruns = 5 * 2048 + 31
@@ -213,10 +213,23 @@ def test_decode_wave_long_runs_in_dense(seed):
     check(a)
 
 
+@pytest.mark.parametrize("at", [0, 4096 * 7 + 11, 300_000 - 200])
+def test_decode_densest_with_long_stretch(at):
+    # random bytes (mean run ~1: 4096-run wave tiles) with a stretch of 200
+    # runs of 255 bytes, so one or two tiles need several 8 KiB windows
+    rng = np.random.default_rng(at + 1)
+    lens = np.ones(300_000, np.int64)
+    lens[at:at + 200] = 255
+    vals = (np.cumsum(rng.integers(1, 255, size=lens.size)) % 256).astype(np.uint8)
+    a = np.repeat(vals, lens)
+    assert a.size <= 2 * lens.size
+    check(a)
+
+
 def test_decode_wave_rejects_zero_count():
     # a zero count inside a dense input (and inside the last, partial tile)
-    for pos in (1000, 2048 * 3 + 5):
-        counts = np.ones(2048 * 3 + 100, np.uint8)
+    for pos in (1000, 4096 * 3 + 5):
+        counts = np.ones(4096 * 3 + 100, np.uint8)
         counts[pos] = 0
         values = (np.arange(counts.size) % 250).astype(np.uint8)
         with pytest.raises(flrl.FLRLError) as e:
