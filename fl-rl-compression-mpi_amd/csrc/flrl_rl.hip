@@ -977,6 +977,48 @@ __global__ __launch_bounds__(kRoThreads, 4) void rl_offsets_kernel(  // 4 workgr
     }
 }
 
+// Bytes [lo, hi) of the 16-byte chunk v (0 <= lo < hi <= 16) stored at dst (16-byte
+// aligned) as naturally aligned pieces: 1, 2, 4, 8 bytes up to a 16-byte
+// boundary, then 8, 4, 2, 1 while they fit.
+__device__ __forceinline__ void store_chunk_part(uint8_t *dst, u32x4 v, uint32_t lo, uint32_t hi)
+{
+    auto dw = [&](uint32_t a) { return a < 8 ? (a < 4 ? v[0] : v[1]) : (a < 12 ? v[2] : v[3]); };
+    auto qw = [&](uint32_t a) {
+        return a < 8 ? ((uint64_t)v[1] << 32) | v[0] : ((uint64_t)v[3] << 32) | v[2];
+    };
+    uint32_t a = lo;
+    if ((a & 1u) && a + 1 <= hi) {
+        dst[a] = (uint8_t)(dw(a) >> (8 * (a & 3)));
+        a += 1;
+    }
+    if ((a & 2u) && a + 2 <= hi) {
+        *reinterpret_cast<uint16_t *>(dst + a) = (uint16_t)(dw(a) >> (8 * (a & 3)));
+        a += 2;
+    }
+    if ((a & 4u) && a + 4 <= hi) {
+        *reinterpret_cast<uint32_t *>(dst + a) = dw(a);
+        a += 4;
+    }
+    if ((a & 8u) && a + 8 <= hi) {
+        *reinterpret_cast<uint64_t *>(dst + a) = qw(a);
+        a += 8;
+    }
+    if (a + 8 <= hi) {
+        *reinterpret_cast<uint64_t *>(dst + a) = qw(a);
+        a += 8;
+    }
+    if (a + 4 <= hi) {
+        *reinterpret_cast<uint32_t *>(dst + a) = dw(a);
+        a += 4;
+    }
+    if (a + 2 <= hi) {
+        *reinterpret_cast<uint16_t *>(dst + a) = (uint16_t)(dw(a) >> (8 * (a & 3)));
+        a += 2;
+    }
+    if (a + 1 <= hi)
+        dst[a] = (uint8_t)(dw(a) >> (8 * (a & 3)));
+}
+
 // ---- decode by rank: output-driven windows ---------------------------------
 // Every lane produces whole 16-byte output chunks, stored coalesced straight
 // from registers. Per kRkWindow-byte window of a tile's output: (1) each run
@@ -1193,7 +1235,7 @@ __global__ __launch_bounds__(kRdThreads) void rl_decode_kernel(
                     }
                     u32x4 o;
                     if (m1 == 0) {
-                        const uint32_t s4 = (uint32_t)s_val[r] * 0x01010101u;
+                        const uint32_t s4 = __builtin_amdgcn_perm(0u, s_val[r], 0u);
                         o = u32x4{s4, s4, s4, s4};
                     } else {
                         // byte i takes run r + k_i, k_i = starts in bytes 1..i (<= 15): the
@@ -1208,25 +1250,26 @@ __global__ __launch_bounds__(kRdThreads) void rl_decode_kernel(
                         const uint32_t w3 = __builtin_amdgcn_alignbyte(d4, d3, sh);
                         // k_i as bytes: s_pfx[x] byte i = popcount of x's bits 0..i (a table:
                         // no 64-bit multiplies); the high half adds the low byte's total
-                        const uint64_t klo = s_pfx[m1 & 0xFFu];
-                        const uint32_t plo = (uint32_t)__popc(m1 & 0xFFu) * 0x01010101u;
-                        const uint64_t khi = s_pfx[m1 >> 8] + (((uint64_t)plo << 32) | plo);
+                        // (no multiplies: v_mul_lo_u32 is a quarter-rate instruction)
+                        const uint64_t klo = s_pfx[m1 & 0xFFu], kh = s_pfx[m1 >> 8];
+                        const uint32_t plo = __builtin_amdgcn_perm(0u, (uint32_t)__popc(m1 & 0xFFu), 0u);
+                        const uint32_t k4[4] = {(uint32_t)klo, (uint32_t)(klo >> 32), (uint32_t)kh + plo,
+                                                (uint32_t)(kh >> 32) + plo};
 #pragma unroll
                         for (int d = 0; d < 4; ++d) {
-                            const uint32_t sel = (uint32_t)((d < 2 ? klo : khi) >> (32 * (d & 1)));
+                            const uint32_t sel = k4[d];
                             const uint32_t lo8 = __builtin_amdgcn_perm(w1, w0, sel & 0x07070707u);
                             const uint32_t hi8 = __builtin_amdgcn_perm(w3, w2, sel & 0x07070707u);
-                            const uint32_t h1 = (sel >> 3) & 0x01010101u;
-                            const uint32_t hm = (h1 << 8) - h1;  // 0xFF where k_i >= 8
-                            o[d] = (hi8 & hm) | (lo8 & ~hm);
+                            // byte i from hi8 (selector 4 + i) where k_i >= 8, else from lo8 (i)
+                            o[d] = __builtin_amdgcn_perm(hi8, lo8, ((sel >> 1) & 0x04040404u) | 0x03020100u);
                         }
                     }
                     if (gp >= cbase && gp + 16 <= cend) {
                         *reinterpret_cast<u32x4 *>(out + gp) = o;  // plain: see the note above
                     } else {  // a chunk shared with a neighbouring tile: its bytes only
-                        for (uint32_t f = 0; f < 16; ++f)
-                            if (gp + f >= cbase && gp + f < cend)
-                                out[gp + f] = (uint8_t)(o[f >> 2] >> (8 * (f & 3)));
+                        const uint32_t lo = gp < cbase ? (uint32_t)(cbase - gp) : 0u;
+                        const uint32_t hi = gp + 16 > cend ? (uint32_t)(cend - gp) : 16u;
+                        store_chunk_part(out + gp, o, lo, hi);
                     }
                 }
                 starts_before += wtot;
@@ -1292,48 +1335,6 @@ __device__ __forceinline__ void wave_lds_sync()
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-// Bytes [lo, hi) of the 16-byte chunk v (0 <= lo < hi <= 16) stored at dst (16-byte
-// aligned) as naturally aligned pieces: 1, 2, 4, 8 bytes up to a 16-byte
-// boundary, then 8, 4, 2, 1 while they fit.
-__device__ __forceinline__ void store_chunk_part(uint8_t *dst, u32x4 v, uint32_t lo, uint32_t hi)
-{
-    auto dw = [&](uint32_t a) { return a < 8 ? (a < 4 ? v[0] : v[1]) : (a < 12 ? v[2] : v[3]); };
-    auto qw = [&](uint32_t a) {
-        return a < 8 ? ((uint64_t)v[1] << 32) | v[0] : ((uint64_t)v[3] << 32) | v[2];
-    };
-    uint32_t a = lo;
-    if ((a & 1u) && a + 1 <= hi) {
-        dst[a] = (uint8_t)(dw(a) >> (8 * (a & 3)));
-        a += 1;
-    }
-    if ((a & 2u) && a + 2 <= hi) {
-        *reinterpret_cast<uint16_t *>(dst + a) = (uint16_t)(dw(a) >> (8 * (a & 3)));
-        a += 2;
-    }
-    if ((a & 4u) && a + 4 <= hi) {
-        *reinterpret_cast<uint32_t *>(dst + a) = dw(a);
-        a += 4;
-    }
-    if ((a & 8u) && a + 8 <= hi) {
-        *reinterpret_cast<uint64_t *>(dst + a) = qw(a);
-        a += 8;
-    }
-    if (a + 8 <= hi) {
-        *reinterpret_cast<uint64_t *>(dst + a) = qw(a);
-        a += 8;
-    }
-    if (a + 4 <= hi) {
-        *reinterpret_cast<uint32_t *>(dst + a) = dw(a);
-        a += 4;
-    }
-    if (a + 2 <= hi) {
-        *reinterpret_cast<uint16_t *>(dst + a) = (uint16_t)(dw(a) >> (8 * (a & 3)));
-        a += 2;
-    }
-    if (a + 1 <= hi)
-        dst[a] = (uint8_t)(dw(a) >> (8 * (a & 3)));
 }
 
 template <int RPL>
