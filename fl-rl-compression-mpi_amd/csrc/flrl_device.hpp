@@ -125,6 +125,11 @@ __device__ __forceinline__ uint32_t wave_shr1(uint32_t v)
     return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xF, 0xF, false);
 }
 
+__device__ __forceinline__ uint64_t wave_shr1_64(uint64_t v)
+{
+    return ((uint64_t)wave_shr1((uint32_t)(v >> 32)) << 32) | wave_shr1((uint32_t)v);
+}
+
 // Inclusive wave scan in six DPP steps (no LDS crossbar round trips):
 // row_shr 1/2/4/8 scan each row, row_bcast:15 and :31 carry row totals up.
 __device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t v)

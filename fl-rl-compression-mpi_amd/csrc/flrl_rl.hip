@@ -832,6 +832,218 @@ __global__ __launch_bounds__(T, FLRL_RL_MINW) void rl_encode_wave_kernel(
     FLRL_RL_TRACE(tile, 4);
 }
 
+// ---- RL encode in three passes (no look-back wait) ---------------------------
+// The single-pass kernel above spends a third of each tile's life waiting in
+// its look-back for the slowest predecessor's scan (trace: DESIGN §9). Here
+// (1) rl_encode_scan_kernel scans every tile independently (grid = tiles, no
+// ticket, no look-back): each wave's chunk summary and the staged runs go to
+// the scratch, the tile's composite map to tmap[tile]; (2) rl_encode_state_kernel
+// scans the tile maps (256 per workgroup, one decoupled look-back per
+// workgroup) into each tile's incoming state (heads before it, chunk state);
+// (3) rl_encode_emit_kernel gives every wave its state (the tile's, advanced by
+// the maps of the waves before it), brings its staged runs back into LDS and
+// emits exactly as the single-pass kernel (split heads, staged runs, re-read
+// sub-chunks past a staging overflow, the final run). Extra traffic: the staged
+// runs out and back (4 bytes per staged run).
+template <int LB, int SUB, int W>
+struct RlChunkSum {  // a wave's Chunk in 48 bytes
+    using Wv = RlWave<LB, SUB, W>;
+    __device__ static void put(u32x4 *dst, const typename Wv::Chunk &C)
+    {
+        dst[0] = u32x4{(uint32_t)C.off, (uint32_t)(C.off >> 32), C.len, (uint32_t)C.ns};
+        dst[1] = u32x4{(uint32_t)C.nst, C.first, C.K, C.Kst};
+        dst[2] = u32x4{C.rel_in, C.rel_st, C.v0, 0u};
+    }
+    __device__ static typename Wv::Chunk get(const u32x4 *src)
+    {
+        typename Wv::Chunk C;
+        const u32x4 a = src[0], b = src[1], c = src[2];
+        C.off = ((uint64_t)a[1] << 32) | a[0];
+        C.len = a[2];
+        C.ns = (int)a[3];
+        C.nst = (int)b[0];
+        C.first = b[1];
+        C.K = b[2];
+        C.Kst = b[3];
+        C.rel_in = c[0];
+        C.rel_st = c[1];
+        C.v0 = c[2];
+        return C;
+    }
+};
+
+template <int T, int LB, int SUB>
+__global__ __launch_bounds__(T) void rl_encode_scan_kernel(const uint8_t *__restrict__ in, uint64_t n,
+                                                           uint64_t *__restrict__ tmap, u32x4 *__restrict__ sums,
+                                                           uint8_t *__restrict__ gstage)
+{
+    constexpr int W = T / kWave;
+    using Wv = RlWave<LB, SUB, W>;
+    __shared__ __attribute__((aligned(16))) uint8_t s_lds[W * Wv::WB + kRlStageBytes];
+    __shared__ uint64_t s_map[W];
+    const int w = threadIdx.x / kWave;
+    const Wv V(in, n, s_lds, w);
+    const uint32_t tile = blockIdx.x;
+    typename Wv::Chunk C;
+    const uint64_t off = (uint64_t)tile * Wv::TBT + (uint64_t)w * Wv::CB;
+    const uint32_t len = off >= n ? 0u : (n - off < (uint64_t)Wv::CB ? (uint32_t)(n - off) : (uint32_t)Wv::CB);
+    V.scan_chunk(off, len, C, [](int) {});
+    uint8_t *gs = gstage + (uint64_t)tile * kRlStageBytes + (uint64_t)w * 2 * Wv::SW;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the staging writes of all lanes first
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    V.staging_to(gs, gs + Wv::SW, C.Kst);
+    if (V.lane == 0) {
+        RlChunkSum<LB, SUB, W>::put(sums + ((uint64_t)tile * W + w) * 3, C);
+        s_map[w] = C.map();
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint64_t m = s_map[0];
+#pragma unroll
+        for (int v = 1; v < W; ++v)
+            m = sm_compose(m, s_map[v]);
+        tmap[tile] = m;
+    }
+}
+
+// inclusive wave scan of segment maps (oldest first; lanes without a source
+// read 0 = the identity map "no natural head, 0 bytes")
+__device__ __forceinline__ uint64_t dpp64_up(uint64_t v, int step)
+{
+    switch (step) {
+    case 0: return ((uint64_t)dpp_up0<0x111, 0xF>((uint32_t)(v >> 32)) << 32) | dpp_up0<0x111, 0xF>((uint32_t)v);
+    case 1: return ((uint64_t)dpp_up0<0x112, 0xF>((uint32_t)(v >> 32)) << 32) | dpp_up0<0x112, 0xF>((uint32_t)v);
+    case 2: return ((uint64_t)dpp_up0<0x114, 0xF>((uint32_t)(v >> 32)) << 32) | dpp_up0<0x114, 0xF>((uint32_t)v);
+    case 3: return ((uint64_t)dpp_up0<0x118, 0xF>((uint32_t)(v >> 32)) << 32) | dpp_up0<0x118, 0xF>((uint32_t)v);
+    case 4: return ((uint64_t)dpp_up0<0x142, 0xA>((uint32_t)(v >> 32)) << 32) | dpp_up0<0x142, 0xA>((uint32_t)v);
+    default: return ((uint64_t)dpp_up0<0x143, 0xC>((uint32_t)(v >> 32)) << 32) | dpp_up0<0x143, 0xC>((uint32_t)v);
+    }
+}
+__device__ __forceinline__ uint64_t wave_incl_scan_sm(uint64_t m)
+{
+#pragma unroll
+    for (int k = 0; k < 6; ++k)
+        m = sm_compose(dpp64_up(m, k), m);
+    return m;
+}
+
+constexpr int kRsThreads = 256;  // tile maps per state-scan workgroup
+
+// Tile states by reduce-then-scan in one launch: every workgroup scans its 256
+// tile maps (packed: <= 32 MiB of input, within the 26-bit fields) into
+// in-block exclusive prefixes (tlocal) and stores its aggregate unpacked
+// (kind, L or pre, K, c); the last workgroup to finish (a counter) applies the
+// aggregates in order to the state (H, c), from (0, 0), and writes each
+// block's incoming state (bpre: H, c). A tile's state is then
+// sm_compose(bpre[tile / 256] as Const, tlocal[tile]) (rl_encode_emit_kernel).
+__global__ __launch_bounds__(kRsThreads) void rl_encode_state_kernel(const uint64_t *__restrict__ tmap,
+                                                                     uint32_t ntiles, uint32_t nblocks,
+                                                                     uint64_t *__restrict__ tlocal,
+                                                                     uint64_t *__restrict__ bagg,
+                                                                     uint64_t *__restrict__ bpre, Ctrl *ctrl)
+{
+    constexpr int NW = kRsThreads / kWave;
+    __shared__ uint64_t s_w[NW];
+    __shared__ uint32_t s_last;
+    const int tid = threadIdx.x;
+    const int lane = tid & (kWave - 1);
+    const int wave = tid / kWave;
+    const uint32_t blk = blockIdx.x;
+    const uint32_t t = blk * kRsThreads + tid;
+    const uint64_t m = t < ntiles ? tmap[t] : sm_nonat(0);
+    const uint64_t inc = wave_incl_scan_sm(m);
+    if (lane == kWave - 1)
+        s_w[wave] = inc;
+    __syncthreads();
+    uint64_t before = sm_nonat(0), agg = sm_nonat(0);  // waves before this one; the whole block
+#pragma unroll
+    for (int v = 0; v < NW; ++v) {
+        const uint64_t x = s_w[v];
+        if (v < wave)
+            before = sm_compose(before, x);
+        agg = sm_compose(agg, x);
+    }
+    if (t < ntiles)
+        tlocal[t] = sm_compose(before, wave_shr1_64(inc));  // lane 0 reads the identity
+    if (tid == 0) {
+        const bool nat = (agg & kSmKind) == kSmNat;
+        bagg[4 * blk + 0] = nat ? 1 : 0;
+        bagg[4 * blk + 1] = sm_a(agg);
+        bagg[4 * blk + 2] = nat ? sm_b(agg) : 0;
+        bagg[4 * blk + 3] = sm_c(agg);
+        __threadfence();  // the aggregate before the count
+        const uint32_t k = atomicAdd(&ctrl->ticket, 1u);
+        if (k >= nblocks)  // the scratch's counter was not reset for this launch
+            raise_error(ctrl, FLRL_E_ARG);
+        s_last = k == nblocks - 1;
+    }
+    __syncthreads();
+    if (!s_last)
+        return;
+    // the last block: every aggregate into LDS (all loads in flight at once, past
+    // the L1), then thread 0 applies them in order
+    __threadfence();  // every block's aggregate is visible
+    __shared__ uint64_t s_agg[kRsThreads][4];
+    uint64_t H = 0;
+    uint32_t c = 0;
+    for (uint32_t b0 = 0; b0 < nblocks; b0 += kRsThreads) {
+        const uint32_t b = b0 + tid;
+        if (b < nblocks) {
+#pragma unroll
+            for (int f = 0; f < 4; ++f)
+                s_agg[tid][f] = granule_load(&bagg[4 * b + f]);
+        }
+        __syncthreads();
+        if (tid == 0) {
+            const uint32_t nb = nblocks - b0 < (uint32_t)kRsThreads ? nblocks - b0 : (uint32_t)kRsThreads;
+            for (uint32_t i = 0; i < nb; ++i) {
+                bpre[2 * (b0 + i)] = H;
+                bpre[2 * (b0 + i) + 1] = c;
+                const uint64_t a = s_agg[i][1];
+                if (s_agg[i][0]) {
+                    H += splits64(c, a) + s_agg[i][2];
+                    c = (uint32_t)s_agg[i][3];
+                } else {
+                    H += splits64(c, a);
+                    c = add_c64(c, a);
+                }
+            }
+        }
+        __syncthreads();
+    }
+}
+
+template <int T, int LB, int SUB>
+__global__ __launch_bounds__(T) void rl_encode_emit_kernel(const uint8_t *__restrict__ in, uint64_t n,
+                                                           const u32x4 *__restrict__ sums,
+                                                           const uint64_t *__restrict__ tlocal,
+                                                           const uint64_t *__restrict__ bpre,
+                                                           const uint8_t *__restrict__ gstage,
+                                                           uint8_t *__restrict__ counts, uint8_t *__restrict__ values,
+                                                           uint64_t *__restrict__ runs_out)
+{
+    constexpr int W = T / kWave;
+    using Wv = RlWave<LB, SUB, W>;
+    using Sum = RlChunkSum<LB, SUB, W>;
+    __shared__ __attribute__((aligned(16))) uint8_t s_lds[W * Wv::WB + kRlStageBytes];
+    const int w = threadIdx.x / kWave;
+    const Wv V(in, n, s_lds, w);
+    const uint32_t tile = blockIdx.x;
+    const u32x4 *ts = sums + (uint64_t)tile * W * 3;
+    const uint32_t sb = tile / kRsThreads;
+    uint64_t st = sm_compose(sm_const(bpre[2 * sb], (uint32_t)bpre[2 * sb + 1]), tlocal[tile]);
+    for (int v = 0; v < w; ++v)
+        st = sm_compose(st, Sum::get(ts + 3 * v).map());
+    const typename Wv::Chunk C = Sum::get(ts + 3 * w);
+    const uint8_t *gs = gstage + (uint64_t)tile * kRlStageBytes + (uint64_t)w * 2 * Wv::SW;
+    V.staging_from(gs, gs + Wv::SW, C.Kst);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    V.emit(C, sm_h(st), sm_c(st), counts, values, runs_out);
+}
+
 // ---- decode pre-pass: output offsets of each decode tile ------------------
 // A workgroup (4 waves) takes a contiguous span of iters x kRoRuns counts by
 // ticket; wave w owns the w-th quarter of it and walks it in steps of 16384
@@ -1519,13 +1731,34 @@ __global__ __launch_bounds__(kWdThreads) void rl_decode_wave_kernel(
     }
 }
 
+#ifndef FLRL_RL_3PASS
+#define FLRL_RL_3PASS 1
+#endif
+constexpr bool kRl3Pass = FLRL_RL_3PASS;
+
+// single pass: [Ctrl][status: tiles] (zeroed); three passes: [Ctrl] (zeroed)
+// [tmap: tiles][tlocal: tiles][bagg: blocks x 32 B][bpre: blocks x 16 B]
+// [sums: tiles x 4 x 48 B][staged runs: tiles x kRlStageBytes]
 struct RlEncLayout {
-    size_t tiles, zero, bytes;
+    size_t tiles, sblocks, zero, o_tmap, o_tstate, o_bagg, o_bpre, o_sums, o_stage, bytes;
     explicit RlEncLayout(size_t n)
     {
         tiles = div_up(n, (size_t)kRlTileBytes);
-        zero = sizeof(Ctrl) + round_up(tiles * 8, 16);  // ticket, error, status granules
-        bytes = zero;
+        if (!kRl3Pass) {
+            sblocks = 0;
+            zero = sizeof(Ctrl) + round_up(tiles * 8, 16);  // ticket, error, status granules
+            o_tmap = o_tstate = o_bagg = o_bpre = o_sums = o_stage = bytes = zero;
+            return;
+        }
+        sblocks = div_up(tiles, (size_t)kRsThreads);
+        zero = sizeof(Ctrl);  // the state kernel's block counter
+        o_tmap = zero;
+        o_tstate = o_tmap + round_up(tiles * 8, 16);   // tlocal
+        o_bagg = o_tstate + round_up(tiles * 8, 16);
+        o_bpre = o_bagg + sblocks * 32;
+        o_sums = o_bpre + sblocks * 16;
+        o_stage = o_sums + tiles * (kRlThreads / kWave) * 48;
+        bytes = o_stage + tiles * (size_t)kRlStageBytes;
     }
 };
 
@@ -1582,6 +1815,26 @@ extern "C" int flrl_rl_encode_device(const uint8_t *d_in, size_t n, uint8_t *d_c
         return set_error(FLRL_E_ARG, "flrl_rl_encode_device: input too large");
     Ctrl *ctrl = static_cast<Ctrl *>(d_scratch);
     uint64_t *status = reinterpret_cast<uint64_t *>(ctrl + 1);
+    if (kRl3Pass) {
+        uint8_t *base = static_cast<uint8_t *>(d_scratch);
+        uint64_t *tmap = reinterpret_cast<uint64_t *>(base + L.o_tmap);
+        uint64_t *tlocal = reinterpret_cast<uint64_t *>(base + L.o_tstate);
+        uint64_t *bagg = reinterpret_cast<uint64_t *>(base + L.o_bagg);
+        uint64_t *bpre = reinterpret_cast<uint64_t *>(base + L.o_bpre);
+        u32x4 *sums = reinterpret_cast<u32x4 *>(base + L.o_sums);
+        uint8_t *stage = base + L.o_stage;
+        kernel_timing_begin(s);  // the hook brackets all three passes
+        hipLaunchKernelGGL((rl_encode_scan_kernel<kRlThreads, kRlLaneBytes, kRlSub>), dim3((uint32_t)L.tiles),
+                           dim3(kRlThreads), 0, s, d_in, (uint64_t)n, tmap, sums, stage);
+        hipLaunchKernelGGL(rl_encode_state_kernel, dim3((uint32_t)L.sblocks), dim3(kRsThreads), 0, s, tmap,
+                           (uint32_t)L.tiles, (uint32_t)L.sblocks, tlocal, bagg, bpre, ctrl);
+        hipLaunchKernelGGL((rl_encode_emit_kernel<kRlThreads, kRlLaneBytes, kRlSub>), dim3((uint32_t)L.tiles),
+                           dim3(kRlThreads), 0, s, d_in, (uint64_t)n, sums, tlocal, bpre, stage, d_counts,
+                           d_values, d_runs);
+        kernel_timing_end(s);
+        FLRL_HIP(hipGetLastError());
+        return FLRL_OK;
+    }
     kernel_timing_begin(s);
     hipLaunchKernelGGL((rl_encode_wave_kernel<kRlThreads, kRlLaneBytes, kRlSub>), dim3((uint32_t)L.tiles),
                        dim3(kRlThreads), 0, s, d_in, (uint64_t)n, (uint32_t)L.tiles, d_counts, d_values,
