@@ -297,6 +297,45 @@ def _rl_timed(x, n: int, steps: int, warmup: int, dev):
     return d, R, ok, t
 
 
+def _rl_encode_alone(x, n: int, steps: int, warmup: int, dev):
+    """mean kernel ms of back-to-back RL encodes of x (no decode between)"""
+    d = RLDevice(n, dev)
+    stream = torch.cuda.current_stream()
+    for _ in range(warmup + 1):
+        d.encode(x)
+    ev = created_events(steps, 2, stream)
+    torch.cuda.synchronize()
+    for k in range(steps):
+        flrl.time_next_kernel(ev[k][0], ev[k][1])
+        d.encode(x)
+    torch.cuda.synchronize()
+    if d.error():
+        raise SystemExit(f"RL device error {d.error()} during the timed encodes")
+    return mean_ms(ev, 0, 1)
+
+
+def rl_encode_forms(x, n: int, R: int, steps: int, warmup: int, dev):
+    """Kernel ms of both RL encode forms (FLRL_RL_ENCODE_PASSES 1 = default,
+    3 = scan/state/emit) in the encode/decode loop and encoding alone: the
+    three-pass form wins alone and loses in the loop."""
+    res = {}
+    old = os.environ.get("FLRL_RL_ENCODE_PASSES")
+    try:
+        for p in ("1", "3"):
+            os.environ["FLRL_RL_ENCODE_PASSES"] = p
+            d, R2, ok, (_, _, enc_k, _) = _rl_timed(x, n, steps, warmup, dev)
+            del d
+            alone = _rl_encode_alone(x, n, steps, warmup, dev)
+            res[p] = {"loop_ms": round(enc_k, 4), "alone_ms": round(alone, 4), "roundtrip": ok and R2 == R}
+            torch.cuda.empty_cache()
+    finally:
+        if old is None:
+            os.environ.pop("FLRL_RL_ENCODE_PASSES", None)
+        else:
+            os.environ["FLRL_RL_ENCODE_PASSES"] = old
+    return res
+
+
 def rl_dense_section(n: int, seed: int, steps: int, warmup: int, dev):
     """RL of n uniform-random bytes (mean run 1.004: the densest input; decode
     takes the wave-tile kernel): kernel and call times, device round trip."""
@@ -338,6 +377,7 @@ def rl_section(n: int, seed: int, steps: int, warmup: int, dev, cpu: bool):
                       "call_frac": round(alg / (dec_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
         "roundtrip": ok,
     }
+    res["rl_encode_forms"] = rl_encode_forms(x, n, R, steps, warmup, dev)
     if cpu:
         import oracle
         a = x.cpu().numpy()

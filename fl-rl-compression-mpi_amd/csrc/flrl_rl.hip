@@ -1731,20 +1731,28 @@ __global__ __launch_bounds__(kWdThreads) void rl_decode_wave_kernel(
     }
 }
 
-#ifndef FLRL_RL_3PASS
-#define FLRL_RL_3PASS 1
-#endif
-constexpr bool kRl3Pass = FLRL_RL_3PASS;
+// Encode passes: 1 (default) or 3, chosen per call by the environment
+// variable FLRL_RL_ENCODE_PASSES (read when the scratch is sized and when the
+// encode is launched, so set it before both). The three-pass form is 15 %
+// faster on runs32 when the input follows other reads, equal when it follows
+// 1 GiB of writes (their dirty lines are written back during its scan pass, which
+// is bandwidth-bound where the single pass waits in look-backs), and 9 % slower
+// inside bench.py's encode/decode loop.
+static bool rl_three_pass()
+{
+    const char *e = getenv("FLRL_RL_ENCODE_PASSES");
+    return e && e[0] == '3';
+}
 
 // single pass: [Ctrl][status: tiles] (zeroed); three passes: [Ctrl] (zeroed)
 // [tmap: tiles][tlocal: tiles][bagg: blocks x 32 B][bpre: blocks x 16 B]
 // [sums: tiles x 4 x 48 B][staged runs: tiles x kRlStageBytes]
 struct RlEncLayout {
     size_t tiles, sblocks, zero, o_tmap, o_tstate, o_bagg, o_bpre, o_sums, o_stage, bytes;
-    explicit RlEncLayout(size_t n)
+    explicit RlEncLayout(size_t n, bool three)
     {
         tiles = div_up(n, (size_t)kRlTileBytes);
-        if (!kRl3Pass) {
+        if (!three) {
             sblocks = 0;
             zero = sizeof(Ctrl) + round_up(tiles * 8, 16);  // ticket, error, status granules
             o_tmap = o_tstate = o_bagg = o_bpre = o_sums = o_stage = bytes = zero;
@@ -1786,7 +1794,7 @@ struct RlDecLayout {
 
 using namespace flrl;
 
-extern "C" size_t flrl_rl_scratch_bytes(size_t n) { return RlEncLayout(n).bytes; }
+extern "C" size_t flrl_rl_scratch_bytes(size_t n) { return RlEncLayout(n, rl_three_pass()).bytes; }
 extern "C" size_t flrl_rl_decode_scratch_bytes(size_t runs) { return RlDecLayout(runs).bytes; }
 
 extern "C" int flrl_rl_encode_device(const uint8_t *d_in, size_t n, uint8_t *d_counts,
@@ -1794,7 +1802,8 @@ extern "C" int flrl_rl_encode_device(const uint8_t *d_in, size_t n, uint8_t *d_c
                                      size_t scratch_bytes, void *stream)
 {
     hipStream_t s = static_cast<hipStream_t>(stream);
-    const RlEncLayout L(n);
+    const bool three = rl_three_pass();
+    const RlEncLayout L(n, three);
     if (!d_runs || !d_scratch)
         return set_error(FLRL_E_ARG, "flrl_rl_encode_device: null runs/scratch");
     if (scratch_bytes < L.bytes)
@@ -1815,7 +1824,7 @@ extern "C" int flrl_rl_encode_device(const uint8_t *d_in, size_t n, uint8_t *d_c
         return set_error(FLRL_E_ARG, "flrl_rl_encode_device: input too large");
     Ctrl *ctrl = static_cast<Ctrl *>(d_scratch);
     uint64_t *status = reinterpret_cast<uint64_t *>(ctrl + 1);
-    if (kRl3Pass) {
+    if (three) {
         uint8_t *base = static_cast<uint8_t *>(d_scratch);
         uint64_t *tmap = reinterpret_cast<uint64_t *>(base + L.o_tmap);
         uint64_t *tlocal = reinterpret_cast<uint64_t *>(base + L.o_tstate);

@@ -45,6 +45,8 @@ def main():
     p.add_argument("--kind", default="")
     p.add_argument("--bytes", type=int, default=1 << 30)
     p.add_argument("--reps", type=int, default=20)
+    p.add_argument("--dirty", type=int, default=0,
+                   help="bytes written by a fill kernel before every timed call (cache state of a real pipeline)")
     a = p.parse_args()
     libs = [load(x) for x in a.libs.split(",")]
     n = a.bytes
@@ -119,8 +121,11 @@ def main():
     print(f"{a.op} {kind} n={n}: outputs of {len(libs)} builds identical", flush=True)
     tot = [0.0] * len(libs)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    dirty = torch.empty(a.dirty, dtype=torch.uint8, device="cuda") if a.dirty else None
     for r in range(a.reps):
         for i, lib in enumerate(libs):
+            if dirty is not None:
+                dirty.fill_(r & 0xFF)
             e0.record()
             call(lib)
             e1.record()

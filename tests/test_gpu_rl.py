@@ -25,6 +25,14 @@ def _need_gpu():
         pytest.fail("GPU tests need a HIP device")
 
 
+@pytest.fixture(params=["1", "3"])
+def passes(request, monkeypatch):
+    """Encode tests run with both encode forms: the single look-back pass
+    (default) and the scan/state/emit passes (FLRL_RL_ENCODE_PASSES=3)."""
+    monkeypatch.setenv("FLRL_RL_ENCODE_PASSES", request.param)
+    return request.param
+
+
 def check(a: np.ndarray):
     r = flrl.rl_compress(a)
     counts, values = oracle.rl_compress(a)
@@ -37,7 +45,7 @@ def check(a: np.ndarray):
     return r
 
 
-def test_kats(golden):
+def test_kats(golden, passes):
     for case in golden["rl_kat"]:
         data = np.frombuffer(kat_input(case), np.uint8)
         r = flrl.rl_compress(data)
@@ -58,13 +66,13 @@ SIZES = [1, 2, 15, 16, 17, 255, 256, 257, 1023, 1024, 1025, 16383, 16384, 16385,
 
 @pytest.mark.parametrize("n", SIZES)
 @pytest.mark.parametrize("kind", ["runs32", "longruns", "u8", "zero"])
-def test_sizes_vs_oracle(n, kind):
+def test_sizes_vs_oracle(n, kind, passes):
     check(oracle.gen(kind, n, 17))
 
 
 @pytest.mark.parametrize("L", [254, 255, 256, 509, 510, 511, 16384 + 3, 131072 + 255, 400_000])
 @pytest.mark.parametrize("start", [0, 1, 15, 16, 1023, 16380, 32767, 32768, 65535, 65536, 98304, 131070])
-def test_long_run_splits(L, start):
+def test_long_run_splits(L, start, passes):
     # one long run of 7s starting at `start` inside random data
     rng = np.random.default_rng(L + start)
     a = rng.integers(0, 256, size=start + L + 300, dtype=np.uint8)
@@ -76,7 +84,7 @@ def test_long_run_splits(L, start):
     check(a)
 
 
-def test_runs_spanning_many_tiles():
+def test_runs_spanning_many_tiles(passes):
     # alternating long runs of 1..3 tiles, so most tiles have no natural head
     parts = []
     rng = np.random.default_rng(3)
@@ -91,7 +99,7 @@ def test_runs_spanning_many_tiles():
 
 
 @pytest.mark.parametrize("quiet", [1, 32768 - 3, 32768 + 100, 65536 - 3, 98304 + 7, 131072 + 5])
-def test_first_natural_head_late(quiet):
+def test_first_natural_head_late(quiet, passes):
     # no natural head for `quiet` bytes (in the first 32 KiB sub-tile, at and
     # after sub-tile boundaries, in the last sub-tile, in the next tile), then
     # mixed data
@@ -103,7 +111,7 @@ def test_first_natural_head_late(quiet):
 
 
 @pytest.mark.parametrize("maxrun", [6, 12, 20, 28, 40])
-def test_medium_density(maxrun):
+def test_medium_density(maxrun, passes):
     # mean runs around the staging threshold (state-independent runs per tile
     # vs the LDS staging capacity): the staging overflows in the first, second,
     # third or last 32 KiB sub-tile of a tile, or not at all
@@ -119,7 +127,7 @@ def test_decode_offsets_rounds():
     check(oracle.gen("u8", (72 << 20) + 999, 23))
 
 
-def test_all_zero_large():
+def test_all_zero_large(passes):
     a = np.zeros(5 * 131072 + 77, np.uint8)  # no natural head after byte 0
     r = check(a)
     assert r.counts.tolist()[:3] == [255, 255, 255]
@@ -135,7 +143,7 @@ def test_decode_rejects_malformed():
         flrl.rl_decompress(3, np.zeros(0, np.uint8), np.zeros(0, np.uint8))
 
 
-def test_device_1gib_runs32():
+def test_device_1gib_runs32(passes):
     """Config #3: RL encode/decode of 1 GiB runs32 (mean run 32) — bit-exact vs
     the oracle over the full buffer and a device round trip."""
     from flrl.device import RLDevice
@@ -237,7 +245,7 @@ def test_decode_wave_rejects_zero_count():
         assert e.value.code == flrl.E_FORMAT
 
 
-def test_device_more_than_2_32_runs():
+def test_device_more_than_2_32_runs(passes):
     """64-bit run indices: ~4.27 GiB of random bytes has R > 2^32 runs (all
     shorter than 255). Device round trip; R against an independent torch count
     of run starts; and the records of three windows that start at run starts
