@@ -47,6 +47,8 @@ def main():
     p.add_argument("--reps", type=int, default=20)
     p.add_argument("--dirty", type=int, default=0,
                    help="bytes written by a fill kernel before every timed call (cache state of a real pipeline)")
+    p.add_argument("--nocheck", action="store_true",
+                   help="timing-only builds: do not compare outputs with the first build's")
     a = p.parse_args()
     libs = [load(x) for x in a.libs.split(",")]
     n = a.bytes
@@ -116,7 +118,7 @@ def main():
             ref = r
             if a.op.endswith("decode"):
                 assert torch.equal(r, x[:n]), "round trip failed"
-        else:
+        elif not a.nocheck:
             assert torch.equal(ref, r), f"build {i} output differs from build 0"
     print(f"{a.op} {kind} n={n}: outputs of {len(libs)} builds identical", flush=True)
     tot = [0.0] * len(libs)
