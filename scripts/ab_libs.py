@@ -47,6 +47,8 @@ def main():
     p.add_argument("--reps", type=int, default=20)
     p.add_argument("--dirty", type=int, default=0,
                    help="bytes written by a fill kernel before every timed call (cache state of a real pipeline)")
+    p.add_argument("--clean", type=int, default=0,
+                   help="bytes read by a reduction before every timed call (evicts dirty cache lines)")
     p.add_argument("--nocheck", action="store_true",
                    help="timing-only builds: do not compare outputs with the first build's")
     a = p.parse_args()
@@ -124,10 +126,13 @@ def main():
     tot = [0.0] * len(libs)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     dirty = torch.empty(a.dirty, dtype=torch.uint8, device="cuda") if a.dirty else None
+    clean = torch.ones(a.clean // 4, dtype=torch.int32, device="cuda") if a.clean else None
     for r in range(a.reps):
         for i, lib in enumerate(libs):
             if dirty is not None:
                 dirty.fill_(r & 0xFF)
+            if clean is not None:
+                torch.amax(clean)
             e0.record()
             call(lib)
             e1.record()

@@ -11,7 +11,7 @@ for spec in $OPS; do
   for k in ${kinds//,/ }; do
     b=""; case $k in *@*) b="--bytes ${k#*@}"; k=${k%@*};; esac
     echo "== $op $k $b"
-    timeout -k 10 120 python3 scripts/ab_libs.py --op "$op" --libs "$LIBS" --kind "$k" $b --reps ${REPS:-20} ${DIRTY:+--dirty $DIRTY} ${NOCHECK:+--nocheck} || exit 1
+    timeout -k 10 120 python3 scripts/ab_libs.py --op "$op" --libs "$LIBS" --kind "$k" $b --reps ${REPS:-20} ${DIRTY:+--dirty $DIRTY} ${NOCHECK:+--nocheck} ${CLEAN:+--clean $CLEAN} || exit 1
   done
 done
 if [ -n "$PYTEST_K" ]; then
