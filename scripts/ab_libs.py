@@ -14,6 +14,7 @@ ops: fl_encode, fl_decode, rl_encode, rl_decode. Inputs: --kind u8|lo4|zero
 import argparse
 import ctypes
 import os
+import random
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -128,7 +129,12 @@ def main():
     dirty = torch.empty(a.dirty, dtype=torch.uint8, device="cuda") if a.dirty else None
     clean = torch.ones(a.clean // 4, dtype=torch.int32, device="cuda") if a.clean else None
     for r in range(a.reps):
-        for i, lib in enumerate(libs):
+        # builds in a shuffled order per rep: the preceding call's cache state
+        # moves a build's time by up to ~4 %, so no build keeps one predecessor
+        order = list(range(len(libs)))
+        random.Random(r).shuffle(order)
+        for i in order:
+            lib = libs[i]
             if dirty is not None:
                 dirty.fill_(r & 0xFF)
             if clean is not None:
