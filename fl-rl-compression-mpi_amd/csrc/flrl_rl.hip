@@ -86,9 +86,15 @@ constexpr int kRlLookG = FLRL_RL_LOOKG;  // look-back granules per lane (window 
 #endif
 constexpr int kRlStageBytes = FLRL_RL_STAGE;  // LDS run staging per workgroup
 
-constexpr int kRdRuns = 4096;        // runs per decode tile
-constexpr int kRdThreads = 256;
-constexpr int kRdPerCU = 4;          // resident decode workgroups per CU (LDS 37 KB each)
+#ifndef FLRL_RD_T
+#define FLRL_RD_T 256
+#endif
+constexpr int kRdThreads = FLRL_RD_T;
+constexpr int kRdRuns = 16 * kRdThreads;  // runs per decode tile
+#ifndef FLRL_RD_PER_CU
+#define FLRL_RD_PER_CU 4
+#endif
+constexpr int kRdPerCU = FLRL_RD_PER_CU;  // resident decode workgroups per CU (LDS 31 KB, 96 VGPRs each)
 
 // ---- PhaseMap packed in a u32: bit 31 = constant, bits 0-30 = value --------
 // The value is kept unreduced (a byte count within one tile, < 2^31) and taken
@@ -1261,7 +1267,7 @@ __global__ __launch_bounds__(kRdThreads) void rl_decode_kernel(
     constexpr int RPT = kRdRuns / T;        // runs per thread
     constexpr int WPT = kRkWords / T;       // bitmap words per thread (scan)
     constexpr int CPT = kRkWindow / 16 / T; // chunks per thread per window
-    static_assert(RPT == 16 && WPT == 8, "one 16-byte count/value vector, two bitmap vectors per thread");
+    static_assert(RPT == 16 && WPT % 4 == 0, "one 16-byte count/value vector, whole bitmap vectors per thread");
     // [bitmap: kRkWords][s_pre: kRkWords][s_st: kRdRuns + 1] u32; a dense tile
     // (output <= kRkDense bytes) uses the same LDS as its byte output window
     __shared__ u32x4 s_big4[(2 * kRkWords + kRdRuns + 1 + 3) / 4];
@@ -1281,8 +1287,8 @@ __global__ __launch_bounds__(kRdThreads) void rl_decode_kernel(
     uint64_t tile = blockIdx.x;
     if (tile >= ntiles)
         return;
-    {
-        static_assert(T == 256, "one table entry per thread");
+    if (tid < 256) {
+        static_assert(T >= 256, "one table entry per thread");
         uint64_t e = 0;
         uint32_t c = 0;
 #pragma unroll
