@@ -86,15 +86,19 @@ constexpr int kRlLookG = FLRL_RL_LOOKG;  // look-back granules per lane (window 
 #endif
 constexpr int kRlStageBytes = FLRL_RL_STAGE;  // LDS run staging per workgroup
 
-#ifndef FLRL_RD_T
-#define FLRL_RD_T 256
+// Block decode workgroups: 512 threads over 8192-run tiles, 2 per CU, unless the
+// mean run is at least kRdNarrowMean bytes (runs near the 255 maximum: little
+// assembly per chunk), then 256 threads over 4096-run tiles, 4 per CU. 1 GiB,
+// 512 vs 256 threads: runs32 -7 %, runs of 1..48 -5 %, 1..256 -8 %, long runs
+// (1..1023 bytes, split) -4 %; all-zero +10 %.
+constexpr int kRdThreads = 256;
+constexpr int kRdThreadsWide = 512;
+#ifndef FLRL_RD_NARROW_MEAN
+#define FLRL_RD_NARROW_MEAN 240
 #endif
-constexpr int kRdThreads = FLRL_RD_T;
-constexpr int kRdRuns = 16 * kRdThreads;  // runs per decode tile
-#ifndef FLRL_RD_PER_CU
-#define FLRL_RD_PER_CU 4
-#endif
-constexpr int kRdPerCU = FLRL_RD_PER_CU;  // resident decode workgroups per CU (LDS 31 KB, 96 VGPRs each)
+constexpr uint64_t kRdNarrowMean = FLRL_RD_NARROW_MEAN;
+template <int T>
+constexpr int rd_per_cu() { return T == 512 ? 2 : 4; }  // LDS-bound: 59 / 31 KB per workgroup
 
 // ---- PhaseMap packed in a u32: bit 31 = constant, bits 0-30 = value --------
 // The value is kept unreduced (a byte count within one tile, < 2^31) and taken
@@ -1259,11 +1263,12 @@ constexpr int kRkWindow = 65536;            // output bytes per window
 constexpr int kRkWords = kRkWindow / 32;    // bitmap words per window
 constexpr int kRkDense = 32768;             // tiles with at most this much output: per-thread memsets
 
-__global__ __launch_bounds__(kRdThreads) void rl_decode_kernel(
+template <int T>
+__global__ __launch_bounds__(T) void rl_decode_kernel(
     const uint8_t *__restrict__ counts, const uint8_t *__restrict__ values, uint64_t runs,
     uint8_t *__restrict__ out, uint64_t n, const uint64_t *__restrict__ tile_base, uint64_t ntiles)
 {
-    constexpr int T = kRdThreads;
+    constexpr int kRdRuns = 16 * T;  // runs per tile
     constexpr int RPT = kRdRuns / T;        // runs per thread
     constexpr int WPT = kRkWords / T;       // bitmap words per thread (scan)
     constexpr int CPT = kRkWindow / 16 / T; // chunks per thread per window
@@ -1783,7 +1788,8 @@ struct RlDecLayout {
     explicit RlDecLayout(size_t runs, size_t n = 0)
     {
         const bool dense = n != 0 && n <= kWdDenseMean * runs;
-        tiles = div_up(runs, (size_t)(dense ? kWdRuns : kRdRuns));
+        const bool wide = n < kRdNarrowMean * runs;
+        tiles = div_up(runs, (size_t)(dense ? kWdRuns : 16 * (wide ? kRdThreadsWide : kRdThreads)));
         // offsets rounds per workgroup: the grid stays within kMaxPrefixBlocks
         iters = div_up(div_up(runs, (size_t)kRoRuns), (size_t)kRoMaxBlocks);
         iters = iters ? iters : 1;
@@ -1920,14 +1926,25 @@ extern "C" int flrl_rl_decode_device(const uint8_t *d_counts, const uint8_t *d_v
         FLRL_HIP(hipGetLastError());
         return FLRL_OK;
     }
-    hipLaunchKernelGGL(rl_offsets_kernel<kRdRuns>, dim3((uint32_t)L.blocks), dim3(kRoThreads), 0, s, d_counts,
-                       (uint64_t)runs, (uint64_t)n, tile_base, (uint32_t)L.tiles,
-                       (uint32_t)L.blocks, (uint32_t)L.iters, ctrl, status);
+    const bool wide = n < kRdNarrowMean * runs;
+    if (wide)
+        hipLaunchKernelGGL(rl_offsets_kernel<16 * kRdThreadsWide>, dim3((uint32_t)L.blocks), dim3(kRoThreads), 0, s,
+                           d_counts, (uint64_t)runs, (uint64_t)n, tile_base, (uint32_t)L.tiles,
+                           (uint32_t)L.blocks, (uint32_t)L.iters, ctrl, status);
+    else
+        hipLaunchKernelGGL(rl_offsets_kernel<16 * kRdThreads>, dim3((uint32_t)L.blocks), dim3(kRoThreads), 0, s,
+                           d_counts, (uint64_t)runs, (uint64_t)n, tile_base, (uint32_t)L.tiles,
+                           (uint32_t)L.blocks, (uint32_t)L.iters, ctrl, status);
     FLRL_HIP(hipGetLastError());
-    const size_t rgrid = (size_t)kRdPerCU * (size_t)cu_count();
+    const size_t rgrid = (size_t)(wide ? rd_per_cu<kRdThreadsWide>() : rd_per_cu<kRdThreads>()) * (size_t)cu_count();
+    const dim3 grid((uint32_t)(L.tiles < rgrid ? L.tiles : rgrid));
     kernel_timing_begin(s);
-    hipLaunchKernelGGL(rl_decode_kernel, dim3((uint32_t)(L.tiles < rgrid ? L.tiles : rgrid)), dim3(kRdThreads), 0,
-                       s, d_counts, d_values, (uint64_t)runs, d_out, (uint64_t)n, tile_base, (uint64_t)L.tiles);
+    if (wide)
+        hipLaunchKernelGGL(rl_decode_kernel<kRdThreadsWide>, grid, dim3(kRdThreadsWide), 0, s, d_counts, d_values,
+                           (uint64_t)runs, d_out, (uint64_t)n, tile_base, (uint64_t)L.tiles);
+    else
+        hipLaunchKernelGGL(rl_decode_kernel<kRdThreads>, grid, dim3(kRdThreads), 0, s, d_counts, d_values,
+                           (uint64_t)runs, d_out, (uint64_t)n, tile_base, (uint64_t)L.tiles);
     kernel_timing_end(s);
     FLRL_HIP(hipGetLastError());
     return FLRL_OK;

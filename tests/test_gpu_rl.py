@@ -165,12 +165,13 @@ def test_device_1gib_runs32(passes):
 
 # ---- rank decode: dense-path threshold (tile output <= 32 KiB), 64 KiB
 # windows, chunks with 0..16 run starts, tiles starting mid-chunk -------------
-@pytest.mark.parametrize("runlen", [7, 8, 9, 15, 16, 17, 24, 31, 33, 63, 64])
+@pytest.mark.parametrize("runlen", [7, 8, 9, 15, 16, 17, 24, 31, 33, 63, 64, 200, 239, 240, 241, 255])
 def test_decode_fixed_run_lengths(runlen):
-    # every tile of 4096 runs has output 4096 * runlen: at, below and above the
-    # dense threshold (8) and the 64 KiB window (16); run starts fall at every
-    # offset within 16-byte chunks when runlen is odd
-    nruns = 3 * 4096 + 77
+    # every tile of 4096 (8192) runs has output 4096 (8192) * runlen: at, below and
+    # above the dense threshold and the 64 KiB window; run starts fall at every
+    # offset within 16-byte chunks when runlen is odd; 239..241 straddle the
+    # 512/256-thread block decode threshold (mean run 240)
+    nruns = 3 * 8192 + 77
     vals = (np.arange(nruns) * 37 % 251 + 1).astype(np.uint8)
     a = np.repeat(vals, runlen)
     check(a[: a.size - 3])
