@@ -1391,19 +1391,21 @@ __global__ __launch_bounds__(T) void rl_decode_kernel(
                 // consecutive runs' start words -- distinct banks, not 16 words apart)
                 // Only the runs that can start in this window: runs before it are
                 // the first starts_before (counts >= 1), and starts are increasing.
+                // Window-relative positions in 32 bits: a tile's output is at most
+                // 16 T x 255 bytes, and the first window starts <= 15 bytes before it.
+                const int32_t tb = (int32_t)(int64_t)(cbase - gw);  // tile start in the window
+                const uint32_t ce = (uint32_t)(cend - gw);          // tile end in the window
                 {
                     for (int k = (int)(starts_before / T); k < RPT; ++k) {
                         const uint32_t j = (uint32_t)(k * T + tid);
                         if (j >= nr)
                             break;
                         const uint32_t x0 = s_st[j], x1 = s_st[j + 1];
-                        const uint64_t p = cbase + x0;
-                        if (p >= gw + kRkWindow)
+                        const int32_t x = tb + (int32_t)x0;
+                        if (x >= kRkWindow)
                             break;
-                        if (x1 > x0 && p >= gw) {
-                            const uint32_t x = (uint32_t)(p - gw);
-                            atomicOr(&s_bm[x >> 5], 1u << (x & 31));
-                        }
+                        if (x1 > x0 && x >= 0)
+                            atomicOr(&s_bm[(uint32_t)x >> 5], 1u << (x & 31));
                     }
                 }
                 __syncthreads();
@@ -1440,12 +1442,14 @@ __global__ __launch_bounds__(T) void rl_decode_kernel(
                 }
                 __syncthreads();
                 // (3) chunks q = k*T + tid: 16 bytes each, coalesced stores
-                const uint64_t wend = cend < gw + kRkWindow ? cend : gw + kRkWindow;
+                const uint32_t wl = ce < (uint32_t)kRkWindow ? ce : (uint32_t)kRkWindow;
+                const uint32_t b0 = tb > 0 ? (uint32_t)tb : 0u;
+                uint8_t *const outw = out + gw;
 #pragma unroll 4
                 for (int k = 0; k < CPT; ++k) {
                     const uint32_t q = (uint32_t)(k * T + tid);
-                    const uint64_t gp = gw + 16ull * q;
-                    if (gp >= wend)
+                    const uint32_t off = 16u * q;
+                    if (off >= wl)
                         break;
                     const uint32_t word = s_bm[q >> 1];
                     const uint32_t m = (q & 1) ? word >> 16 : word & 0xFFFFu;
@@ -1456,11 +1460,10 @@ __global__ __launch_bounds__(T) void rl_decode_kernel(
                         m1 &= m1 - 1;
                         r = 0;
                     }
+                    // (no separate path for chunks without an inner start, m1 = 0: a wave
+                    // almost always holds both kinds, so it would run both; -2 %)
                     u32x4 o;
-                    if (m1 == 0) {
-                        const uint32_t s4 = __builtin_amdgcn_perm(0u, s_val[r], 0u);
-                        o = u32x4{s4, s4, s4, s4};
-                    } else {
+                    {
                         // byte i takes run r + k_i, k_i = starts in bytes 1..i (<= 15): the
                         // 16 values from run r on are gathered with byte permutes
                         const uint32_t *v32 = reinterpret_cast<const uint32_t *>(s_val4);
@@ -1487,12 +1490,12 @@ __global__ __launch_bounds__(T) void rl_decode_kernel(
                             o[d] = __builtin_amdgcn_perm(hi8, lo8, ((sel >> 1) & 0x04040404u) | 0x03020100u);
                         }
                     }
-                    if (gp >= cbase && gp + 16 <= cend) {
-                        *reinterpret_cast<u32x4 *>(out + gp) = o;  // plain: see the note above
+                    if (off >= b0 && off + 16 <= ce) {
+                        *reinterpret_cast<u32x4 *>(outw + off) = o;  // plain: see the note above
                     } else {  // a chunk shared with a neighbouring tile: its bytes only
-                        const uint32_t lo = gp < cbase ? (uint32_t)(cbase - gp) : 0u;
-                        const uint32_t hi = gp + 16 > cend ? (uint32_t)(cend - gp) : 16u;
-                        store_chunk_part(out + gp, o, lo, hi);
+                        const uint32_t lo = off < b0 ? b0 - off : 0u;
+                        const uint32_t hi = off + 16 > ce ? ce - off : 16u;
+                        store_chunk_part(outw + off, o, lo, hi);
                     }
                 }
                 starts_before += wtot;
