@@ -1284,7 +1284,6 @@ __global__ __launch_bounds__(T) void rl_decode_kernel(
     uint32_t *const s_bm = reinterpret_cast<uint32_t *>(s_big4);
     uint32_t *const s_pre = s_bm + kRkWords;  // runs starting in the window before word w
     uint32_t *const s_st = s_pre + kRkWords;  // tile-local start of each run (+ the tile's total)
-    const uint8_t *s_val = reinterpret_cast<const uint8_t *>(s_val4);
     const int tid = threadIdx.x;
     const int lane = tid & (kWave - 1);
     const int wave = tid / kWave;
