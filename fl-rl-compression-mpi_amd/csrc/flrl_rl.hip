@@ -1700,10 +1700,7 @@ __global__ __launch_bounds__(kWdThreads) void rl_decode_wave_kernel(
                         r = 0;
                     }
                     u32x4 ov;
-                    if (m1 == 0) {
-                        const uint32_t s4 = __builtin_amdgcn_perm(0u, reinterpret_cast<const uint8_t *>(sv32)[r], 0u);
-                        ov = u32x4{s4, s4, s4, s4};
-                    } else {
+                    {  // (every chunk takes the permute path, as in the block decode)
                         // byte i takes run r + k_i, k_i = starts in bytes 1..i (<= 15)
                         const uint32_t a = (uint32_t)r >> 2, sh = (uint32_t)r & 3u;
                         const uint32_t d0 = sv32[a], d1 = sv32[a + 1], d2 = sv32[a + 2], d3 = sv32[a + 3],
