@@ -201,8 +201,8 @@ def test_decode_all_starts_in_chunk():
     check(a)
 
 
-# ---- wave decode (mean run <= 24 bytes: one wave per 2048-run tile) --------
-@pytest.mark.parametrize("runlen", [1, 2, 3, 23, 24, 25])
+# ---- wave decode (mean run <= 12 bytes: one wave per 2048-run tile) --------
+@pytest.mark.parametrize("runlen", [1, 2, 3, 11, 12, 13, 23, 24, 25])
 def test_decode_wave_threshold(runlen):
     # mean run exactly at, below and above the wave-decode threshold
     nruns = 5 * 2048 + 31
@@ -215,10 +215,10 @@ def test_decode_wave_long_runs_in_dense(seed):
     # mostly 1-byte runs with a few runs of 100..255 bytes: a dense input (wave
     # decode) whose tiles have one to six 8 KiB output windows
     rng = np.random.default_rng(seed)
-    lens = np.where(rng.random(300_000) < 0.08, rng.integers(100, 256, 300_000), 1)
+    lens = np.where(rng.random(300_000) < 0.04, rng.integers(100, 256, 300_000), 1)
     vals = (np.cumsum(rng.integers(1, 255, size=lens.size)) % 256).astype(np.uint8)
     a = np.repeat(vals, lens)
-    assert a.size <= 24 * lens.size
+    assert a.size <= 12 * lens.size
     check(a)
 
 
