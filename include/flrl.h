@@ -237,7 +237,10 @@ int flrl_rl_decompress(size_t output_size, const uint8_t *counts, const uint8_t 
                        size_t runs, uint8_t **out, size_t *out_size);
 
 /* ---- RL, device-resident (asynchronous) ----------------------------------
- * d_counts / d_values capacity n bytes each; d_runs receives R (device u64). */
+ * d_counts / d_values capacity n bytes each; d_runs receives R (device u64).
+ * The encode runs one look-back pass by default; with the environment variable
+ * FLRL_RL_ENCODE_PASSES=3 it runs scan / state / emit passes instead (same
+ * output; a larger scratch, so set it before sizing the scratch). */
 size_t flrl_rl_scratch_bytes(size_t n);
 int flrl_rl_encode_device(const uint8_t *d_in, size_t n, uint8_t *d_counts, uint8_t *d_values,
                           uint64_t *d_runs, void *d_scratch, size_t scratch_bytes, void *stream);
