@@ -95,3 +95,19 @@ def test_scratch_sizes_monotone():
     for f in (flrl.rl_decode_scratch_bytes, flrl.rl_scratch_bytes, flrl.fl_scratch_bytes):
         sizes = [f(x) for x in pts]
         assert sizes == sorted(sizes), f.__name__
+
+
+@pytest.mark.parametrize("passes", ["1", "3"])
+def test_rl_encode_scratch_per_form(passes, monkeypatch):
+    # FLRL_RL_ENCODE_PASSES picks the encode form when the scratch is sized:
+    # the three-pass form stages runs in the scratch (about 12 % of n), the
+    # single pass needs only its tile states; both grow with n
+    monkeypatch.setenv("FLRL_RL_ENCODE_PASSES", passes)
+    pts = [1, 4096, 131072, 131073, 10 ** 6, 1 << 30]
+    sizes = [flrl.rl_scratch_bytes(x) for x in pts]
+    assert sizes == sorted(sizes)
+    big = flrl.rl_scratch_bytes(1 << 30)
+    if passes == "3":
+        assert (1 << 30) // 10 < big < (1 << 30) // 5
+    else:
+        assert big < (1 << 30) // 100
