@@ -25,9 +25,14 @@ def test_exports_are_c_linkage():
         assert s in exported, s
 
 
-def test_gfx950_code_object():
-    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", flrl.LIB_PATH],
-                         capture_output=True, text=True)
+def test_gfx950_code_object(tmp_path):
+    # llvm-objdump --offloading extracts the code objects next to its input:
+    # run it on a copy so nothing lands beside the shipped library
+    import shutil
+    lib = tmp_path / "libflrl.so"
+    shutil.copy(flrl.LIB_PATH, lib)
+    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", str(lib)],
+                         capture_output=True, text=True, cwd=tmp_path)
     text = out.stdout + out.stderr
     if "gfx950" not in text:  # older objdump: fall back to the bundle string
         with open(flrl.LIB_PATH, "rb") as f:
