@@ -13,10 +13,11 @@ Default workload = BASELINE.json configs[1]: FL encode/decode of 1 GiB of
 uniform-random bytes per GPU, bit-exact against the reference fl-cpu (the
 1 GiB output's sha256 is the reference's).
 
-Every N-rank line also carries `configs4`: BASELINE configs[4], FL encode of
-16 GiB uniform-random bytes per GPU through flrl_fl_encode_rank (encode + the
-RCCL size exchange), 128 GiB at N = 8. At N = 1 the same workload is the
-`north_star` section.
+Every N-rank line (N > 1; at N = 1 with --force-scan) also carries `configs4`:
+BASELINE configs[4], FL encode of 16 GiB uniform-random bytes per GPU through
+flrl_fl_encode_rank (encode + the RCCL size exchange), 128 GiB at N = 8
+(--configs4-bytes sets the per-GPU size). At N = 1 the same bytes without the
+exchange are the `north_star` section.
 
 Launch: python bench.py [--gpus N --steps K --warmup W]. For N > 1 the ranks
 are started by this script (torch.distributed.run child, one rank per GPU)
@@ -93,7 +94,11 @@ def parse():
     p.add_argument("--traffic-json", default=None,
                    help="PMC summary (scripts/summarize_profile.py); default profiles/traffic_<kind>_<bytes>.json")
     p.add_argument("--no-north-star", action="store_true",
-                   help="skip the 16 GiB-per-GPU u8 FL encode (north star at N=1, configs[4] at N>1)")
+                   help="skip the 16 GiB u8 FL encode of the north star (N=1)")
+    p.add_argument("--no-configs4", action="store_true",
+                   help="skip the configs[4] section (16 GiB per GPU through flrl_fl_encode_rank)")
+    p.add_argument("--configs4-bytes", type=int, default=16 << 30,
+                   help="bytes per GPU of the configs[4] section (runs at N>1, and at N=1 with --force-scan)")
     p.add_argument("--no-rl-dense", action="store_true",
                    help="skip the random-bytes RL section (profiles average kernels per name)")
     p.add_argument("--no-rl", action="store_true",
@@ -400,15 +405,30 @@ def rl_section(n: int, seed: int, steps: int, warmup: int, dev, cpu: bool):
     return res
 
 
-def configs4_section(comm, rank: int, world: int, seed: int, steps: int, warmup: int, dev):
+def _barrier(world: int):
+    if world > 1:
+        dist.barrier()
+
+
+def _all_gather_obj(obj, world: int) -> list:
+    if world == 1:
+        return [obj]
+    out = [None] * world
+    dist.all_gather_object(out, obj)
+    return out
+
+
+def configs4_section(comm, rank: int, world: int, seed: int, steps: int, warmup: int, dev,
+                     n: int = 16 << 30):
     """BASELINE configs[4]: FL encode of 16 GiB uniform-random bytes per GPU
-    (128 GiB at N = 8), rank r holding global bytes [r*16 GiB, (r+1)*16 GiB),
-    through flrl_fl_encode_rank (encode + the RCCL all-gather of {F_r, V_r} +
-    device scan). K uninstrumented steps between barriers, max over ranks; then
-    K steps with HIP events around each rank's encode kernel. Parity: every
+    (128 GiB at N = 8), rank r holding global bytes [r*n, (r+1)*n), through
+    flrl_fl_encode_rank (encode + the RCCL all-gather of {F_r, V_r} + device
+    scan). K uninstrumented steps between barriers, max over ranks; then K
+    steps with HIP events around each rank's encode kernel. Parity: every
     rank's device round trip, every rank's exchange record against the ranks'
-    sizes, and rank 0's first 1 GiB against the reference fl-cpu hash."""
-    n = 16 << 30
+    sizes (recomputed by the shipped layout code, flrl_shard_scan), and rank
+    0's first 1 GiB against the reference fl-cpu hash. At N = 1 (with
+    --force-scan) the same path runs on a one-rank communicator."""
     x = gen("u8", n, seed, word_offset=rank * n // 8, device=dev)
     codec = FLDevice(n, dev)
     stream = torch.cuda.current_stream()
@@ -417,13 +437,13 @@ def configs4_section(comm, rank: int, world: int, seed: int, steps: int, warmup:
     torch.cuda.synchronize()
     rec = [int(t) for t in codec.rank_sizes[:flrl.SZ_COUNT].cpu()]
     err = codec.error()
-    dist.barrier()
+    _barrier(world)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(steps):
         codec.encode_rank(comm, x)
     torch.cuda.synchronize()
-    dist.barrier()
+    _barrier(world)
     wall = time.perf_counter() - t0
     ev = created_events(steps, 2, stream)
     torch.cuda.synchronize()
@@ -434,7 +454,7 @@ def configs4_section(comm, rank: int, world: int, seed: int, steps: int, warmup:
     enc_ms = mean_ms(ev, 0, 1)
     v = rec[flrl.SZ_V]
     prefix_ok = None
-    if rank == 0:
+    if rank == 0 and n >= 1 << 30:
         f1 = (1 << 30) // 128
         v1 = int(codec.bits[:f1].to(torch.int64).sum().item()) * 16
         h = hashlib.sha256(struct.pack("<QQQ", 1 << 30, f1, v1))
@@ -450,20 +470,27 @@ def configs4_section(comm, rank: int, world: int, seed: int, steps: int, warmup:
             "F_off": rec[flrl.SZ_F_OFF], "V_off": rec[flrl.SZ_V_OFF],
             "F_total": rec[flrl.SZ_F_TOTAL], "V_total": rec[flrl.SZ_V_TOTAL],
             "frac": alg / (enc_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, "roundtrip": ok}
-    allr = [None] * world
-    dist.all_gather_object(allr, mine)
+    allr = _all_gather_obj(mine, world)
     del x, codec
     torch.cuda.empty_cache()
     if rank != 0:
         return None
     Fs = [r["F"] for r in allr]
     Vs = [r["V"] for r in allr]
+    gathered = np.zeros(2 * world, dtype=np.uint64)  # the exchange's slots, as RCCL filled them
+    for i in range(world):
+        s0 = flrl.shard_slot(i, world, world)
+        gathered[s0], gathered[s0 + 1] = flrl.shard_size_word(n), Vs[i]
     scan_ok = all(r["F_off"] == sum(Fs[:i]) and r["V_off"] == sum(Vs[:i]) and r["F_total"] == sum(Fs)
-                  and r["V_total"] == sum(Vs) and r["F"] == n // 128 for i, r in enumerate(allr))
+                  and r["V_total"] == sum(Vs) and r["F"] == n // 128
+                  and flrl.shard_scan(gathered, world, world, i) == [
+                      r["F"], r["V"], r["F_off"], r["V_off"], r["F_total"], r["V_total"]]
+                  for i, r in enumerate(allr))
     wall = max(r["wall"] for r in allr)
     return {
-        "workload": f"BASELINE configs[4]: FL encode of {n} u8 bytes per GPU x{world} = {n * world} bytes "
-                    f"(seed {seed}), flrl_fl_encode_rank (encode + RCCL size exchange)",
+        "workload": f"{'BASELINE configs[4]' if n == 16 << 30 else 'configs[4] path, custom size'}: FL encode "
+                    f"of {n} u8 bytes per GPU x{world} = {n * world} bytes (seed {seed}), flrl_fl_encode_rank "
+                    f"(encode + RCCL size exchange)",
         "ranks_seen": world,
         "value": round(world * n / (wall / steps) / 1e9, 2),
         "unit": "GB/s (input bytes, whole job)",
@@ -627,8 +654,11 @@ def main():
     torch.cuda.empty_cache()
 
     c4 = None
-    if world > 1 and not args.no_north_star:
-        c4 = configs4_section(comm, rank, world, args.seed, args.steps, args.warmup, dev)
+    if scan and not args.no_configs4:
+        if args.configs4_bytes <= 0 or args.configs4_bytes % 128:
+            raise SystemExit("--configs4-bytes must be a positive multiple of 128")
+        c4 = configs4_section(comm, rank, world, args.seed, args.steps, args.warmup, dev,
+                              n=args.configs4_bytes)
 
     if rank == 0:
         cpu = None

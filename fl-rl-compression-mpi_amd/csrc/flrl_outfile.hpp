@@ -6,11 +6,15 @@
 // paths here read the input while writing, so they write to a temporary file
 // next to the output (same directory, so rename() is atomic on one file
 // system) and rename it into place only on success; on failure the temporary
-// is unlinked and a pre-existing output is untouched. An existing output that
-// is not a regular file (/dev/null, a FIFO) is written directly.
+// is unlinked and a pre-existing output is untouched. The replacement keeps
+// an existing output's mode (and owner where permitted), and a symlinked
+// output's target is replaced, not the link. An existing output that is not a
+// regular file (/dev/null, a FIFO) is written directly, and so is one whose
+// directory does not allow a temporary (unless it is the input being read).
 // Header-only (POSIX), shared by libflrl.so and the CLI.
 #pragma once
 
+#include <errno.h>
 #include <fcntl.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -56,14 +60,22 @@ public:
             ::unlink(tmp_.c_str());
     }
 
-    // false (errno set) when the output cannot be created
-    bool open(const char *path, bool read_write = false)
+    // false (errno set) when the output cannot be created. input_fd: a file the
+    // caller is still reading (never truncated in place, see below), or -1.
+    bool open(const char *path, bool read_write = false, int input_fd = -1)
     {
         path_ = path;
+        // an existing symlink's target is replaced, not the link itself (as
+        // fopen(path, "wb") writes through it)
+        if (char *rp = ::realpath(path, nullptr)) {
+            path_ = rp;
+            ::free(rp);
+        }
         struct stat st;
-        if (::stat(path, &st) == 0 && !S_ISREG(st.st_mode)) {
+        const bool exists = ::stat(path_.c_str(), &st) == 0;
+        if (exists && !S_ISREG(st.st_mode)) {
             direct_ = true;
-            fd = ::open(path, read_write ? O_RDWR : O_WRONLY);
+            fd = ::open(path_.c_str(), read_write ? O_RDWR : O_WRONLY);
             return fd >= 0;
         }
         const size_t slash = path_.rfind('/');
@@ -73,15 +85,37 @@ public:
         std::vector<char> buf(t.begin(), t.end());
         buf.push_back('\0');
         fd = ::mkstemp(buf.data());
-        if (fd < 0)
+        if (fd < 0) {
+            // no temporary possible (directory not writable): truncate and write
+            // the existing output in place, as the reference does — unless it is
+            // the input still being read
+            const int e = errno;
+            struct stat ist;
+            const bool is_input = input_fd >= 0 && ::fstat(input_fd, &ist) == 0 && ist.st_dev == st.st_dev &&
+                                  ist.st_ino == st.st_ino;
+            if (exists && (e == EACCES || e == EPERM || e == EROFS) && !is_input) {
+                fd = ::open(path_.c_str(), (read_write ? O_RDWR : O_WRONLY) | O_TRUNC);
+                if (fd >= 0) {
+                    direct_ = in_place_ = true;
+                    return true;
+                }
+            }
+            errno = e;
             return false;
+        }
         tmp_ = buf.data();
-        (void)::fchmod(fd, new_file_mode());
+        if (exists) {  // the replacement keeps the output's mode and, where allowed, owner
+            (void)::fchmod(fd, st.st_mode & 07777);
+            if (::fchown(fd, st.st_uid, st.st_gid) != 0)
+                (void)::fchmod(fd, st.st_mode & 0777);  // no set-id bits under another owner
+        } else {
+            (void)::fchmod(fd, new_file_mode());
+        }
         return true;
     }
 
     // set the file length (no-op for a non-regular output)
-    bool truncate(uint64_t len) { return direct_ || ::ftruncate(fd, (off_t)len) == 0; }
+    bool truncate(uint64_t len) { return (direct_ && !in_place_) || ::ftruncate(fd, (off_t)len) == 0; }
 
     // close (unless the caller already did, fd = -1) and move into place;
     // false (nothing replaced) on failure
@@ -101,7 +135,7 @@ public:
 
 private:
     std::string path_, tmp_;
-    bool direct_ = false, done_ = false;
+    bool direct_ = false, in_place_ = false, done_ = false;
 };
 
 // An anonymous scratch file in the directory of `near_path` (unlinked at once,

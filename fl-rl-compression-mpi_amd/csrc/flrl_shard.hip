@@ -37,6 +37,7 @@
 #include "flrl.h"
 #include "flrl_device.hpp"
 #include "flrl_internal.hpp"
+#include "flrl_shard_layout.hpp"
 
 using namespace flrl;
 
@@ -49,6 +50,7 @@ struct LocalOuts {
     uint32_t count;
     uint32_t index[kMaxLocal];   // global shard index
     uint64_t *sizes[kMaxLocal];  // its d_sizes (FLRL_SZ_COUNT u64)
+    Ctrl *ctrl[kMaxLocal];       // its scratch (error word)
 };
 
 __global__ void put_u64_kernel(uint64_t *p, uint64_t v)
@@ -57,36 +59,16 @@ __global__ void put_u64_kernel(uint64_t *p, uint64_t v)
         *p = v;
 }
 
-// gather holds {F, V} of shard r at slot ((r % ndev) * S + r / ndev) * 2 (the
-// all-gathered per-device slot arrays). Each thread owns one local shard: its
-// exclusive prefix over shards 0..r-1 in global order, and the totals.
+// Each thread owns one local shard: its record from the all-gathered slots
+// (shard_record, flrl_shard_layout.hpp: the layout the CPU tests check through
+// flrl_shard_scan); a ragged shard before the last raises FLRL_E_ARG in that
+// shard's scratch error word.
 __global__ __launch_bounds__(kWave) void size_scan_kernel(const uint64_t *gather, uint32_t nshards,
                                                           uint32_t ndev, uint32_t S, LocalOuts outs)
 {
-    const uint32_t t = threadIdx.x;
-    for (uint32_t i = t; i < outs.count; i += blockDim.x) {
-        const uint32_t me = outs.index[i];
-        uint64_t F = 0, V = 0, Fo = 0, Vo = 0, Fr = 0, Vr = 0;
-        for (uint32_t r = 0; r < nshards; ++r) {
-            const uint64_t *g = gather + ((uint64_t)(r % ndev) * S + r / ndev) * 2;
-            const uint64_t f = g[0], v = g[1];
-            if (r == me) {
-                Fo = F;
-                Vo = V;
-                Fr = f;
-                Vr = v;
-            }
-            F += f;
-            V += v;
-        }
-        uint64_t *o = outs.sizes[i];
-        o[FLRL_SZ_F] = Fr;
-        o[FLRL_SZ_V] = Vr;
-        o[FLRL_SZ_F_OFF] = Fo;
-        o[FLRL_SZ_V_OFF] = Vo;
-        o[FLRL_SZ_F_TOTAL] = F;
-        o[FLRL_SZ_V_TOTAL] = V;
-    }
+    for (uint32_t i = threadIdx.x; i < outs.count; i += blockDim.x)
+        if (!shard_record(gather, nshards, ndev, S, outs.index[i], outs.sizes[i]))
+            raise_error(outs.ctrl[i], FLRL_E_ARG);
 }
 
 struct Dev {
@@ -335,6 +317,40 @@ extern "C" int flrl_comm_query(const flrl_comm *c, int *nranks, int *rank, int *
     return FLRL_OK;
 }
 
+// ---- the exchange layout on the host (flrl_shard_layout.hpp) ---------------
+
+extern "C" int flrl_shard_range(size_t n, int nshards, int shard, size_t *start, size_t *length)
+{
+    if (nshards <= 0 || shard < 0 || shard >= nshards || !start || !length)
+        return set_error(FLRL_E_ARG, "flrl_shard_range: shard %d of %d", shard, nshards);
+    uint64_t s0 = 0, len = 0;
+    shard_range(n, (uint64_t)nshards, (uint64_t)shard, &s0, &len);
+    *start = s0;
+    *length = len;
+    return FLRL_OK;
+}
+
+extern "C" size_t flrl_shard_slot(int shard, int nshards, int ndev)
+{
+    if (nshards <= 0 || ndev <= 0 || shard < 0 || shard >= nshards)
+        return (size_t)-1;
+    return shard_slot((uint64_t)shard, (uint64_t)ndev, div_up((size_t)nshards, (size_t)ndev));
+}
+
+extern "C" uint64_t flrl_shard_size_word(size_t n) { return shard_f_word(n); }
+
+extern "C" int flrl_shard_scan(const uint64_t *gather, int nshards, int ndev, int shard, uint64_t *rec)
+{
+    clear_error();
+    if (!gather || !rec || nshards <= 0 || ndev <= 0 || shard < 0 || shard >= nshards)
+        return set_error(FLRL_E_ARG, "flrl_shard_scan: shard %d of %d on %d devices", shard, nshards, ndev);
+    const uint32_t S = (uint32_t)div_up((size_t)nshards, (size_t)ndev);
+    if (!shard_record(gather, (uint32_t)nshards, (uint32_t)ndev, S, (uint32_t)shard, rec))
+        return set_error(FLRL_E_ARG, "flrl_shard_scan: a shard before the last is not a multiple of %d bytes",
+                         kFrame);
+    return FLRL_OK;
+}
+
 // ---- device-resident encode + exchange ------------------------------------
 
 extern "C" int flrl_fl_encode_rank(flrl_comm *c, const uint8_t *d_in, size_t n, uint8_t *d_bits,
@@ -356,8 +372,8 @@ extern "C" int flrl_fl_encode_rank(flrl_comm *c, const uint8_t *d_in, size_t n, 
     hipStream_t s = static_cast<hipStream_t>(stream);
     // the previous call's scan may still read the gather array on another stream
     FLRL_HIP(hipStreamWaitEvent(s, d.cdone, 0));
-    uint64_t *slot = d.gather + 2 * (size_t)c->rank;
-    hipLaunchKernelGGL(put_u64_kernel, dim3(1), dim3(kWave), 0, s, slot, (uint64_t)div_up(n, kFrame));
+    uint64_t *slot = d.gather + shard_slot((uint64_t)c->rank, (uint64_t)c->nranks, 1);
+    hipLaunchKernelGGL(put_u64_kernel, dim3(1), dim3(kWave), 0, s, slot, shard_f_word(n));
     FLRL_HIP(hipGetLastError());
     int rc = flrl_fl_encode_device(d_in, n, d_bits, d_values, slot + 1, d_scratch, scratch_bytes, stream);
     if (rc)
@@ -369,6 +385,7 @@ extern "C" int flrl_fl_encode_rank(flrl_comm *c, const uint8_t *d_in, size_t n, 
     outs.count = 1;
     outs.index[0] = (uint32_t)c->rank;
     outs.sizes[0] = d_sizes;
+    outs.ctrl[0] = static_cast<Ctrl *>(d_scratch);
     hipLaunchKernelGGL(size_scan_kernel, dim3(1), dim3(kWave), 0, s, d.gather, (uint32_t)c->nranks,
                        (uint32_t)c->nranks, 1u, outs);
     FLRL_HIP(hipGetLastError());
@@ -395,6 +412,11 @@ extern "C" int flrl_fl_encode_sharded(flrl_comm *c, int nshards, const uint8_t *
     if (S > (size_t)kMaxLocal)
         return set_error(FLRL_E_ARG, "flrl_fl_encode_sharded: %d shards on %zu devices (max %d per device)",
                          nshards, ndev, kMaxLocal);
+    for (size_t r = 0; r + 1 < P; ++r)
+        if (n[r] % kFrame)
+            return set_error(FLRL_E_ARG,
+                             "flrl_fl_encode_sharded: shard %zu has %zu bytes (every shard but the last "
+                             "must be a multiple of %d)", r, n[r], kFrame);
     const int prev = current_device();
     // buffers of shard r must live on device r mod ndev
     for (size_t r = 0; r < P; ++r) {
@@ -422,7 +444,7 @@ extern "C" int flrl_fl_encode_sharded(flrl_comm *c, int nshards, const uint8_t *
     // 1. every shard: F into its slot, encode (V lands in the slot), event
     for (size_t r = 0; r < P && rc == FLRL_OK; ++r) {
         Dev &d = c->dev[r % ndev];
-        const size_t slot_i = ((r % ndev) * S + r / ndev) * 2;
+        const size_t slot_i = shard_slot(r, ndev, S);
         hipStream_t s = static_cast<hipStream_t>(streams[r]);
         if (hipSetDevice(d.id) != hipSuccess) {
             rc = set_error(FLRL_E_HIP, "hipSetDevice(%d) failed", d.id);
@@ -434,7 +456,7 @@ extern "C" int flrl_fl_encode_sharded(flrl_comm *c, int nshards, const uint8_t *
             break;
         }
         hipLaunchKernelGGL(put_u64_kernel, dim3(1), dim3(kWave), 0, s, d.gather + slot_i,
-                           (uint64_t)div_up(n[r], kFrame));
+                           shard_f_word(n[r]));
         if (hipGetLastError() != hipSuccess) {
             rc = set_error(FLRL_E_HIP, "flrl_fl_encode_sharded: launch failed on device %d", d.id);
             break;
@@ -465,6 +487,7 @@ extern "C" int flrl_fl_encode_sharded(flrl_comm *c, int nshards, const uint8_t *
         for (size_t r = k; r < P; r += ndev) {
             outs.index[outs.count] = (uint32_t)r;
             outs.sizes[outs.count] = d_sizes[r];
+            outs.ctrl[outs.count] = static_cast<Ctrl *>(d_scratch[r]);
             ++outs.count;
         }
         if (hipSetDevice(d.id) != hipSuccess) {
@@ -591,7 +614,6 @@ extern "C" int flrl_fl_compress_sharded(const uint8_t *data, size_t size, int ns
     // the reference shard rule (file_io.cu:46-51), size_t: every shard but the
     // last is floor(N/(128P))*128 bytes
     const size_t P = (size_t)nshards;
-    const size_t per = (size / (kFrame * P)) * kFrame;
     std::vector<ShardBufs> sb(P);
     std::vector<const uint8_t *> in(P);
     std::vector<size_t> len(P), scr_b(P);
@@ -599,11 +621,12 @@ extern "C" int flrl_fl_compress_sharded(const uint8_t *data, size_t size, int ns
     std::vector<uint64_t *> sizes(P);
     std::vector<void *> scr(P), streams(P);
     for (size_t r = 0; r < P && rc == FLRL_OK; ++r) {
-        const size_t L = r + 1 == P ? size - (P - 1) * per : per;
+        uint64_t start = 0, L = 0;
+        shard_range(size, P, r, &start, &L);
         rc = sb[r].alloc(c->dev[r % (size_t)ndev].id, L);
         if (rc)
             break;
-        sb[r].off = r * per;
+        sb[r].off = start;
         if (L && hipMemcpyAsync(sb[r].in, data + sb[r].off, L, hipMemcpyHostToDevice, sb[r].s) != hipSuccess)
             rc = set_error(FLRL_E_HIP, "shard %zu upload failed", r);
         in[r] = sb[r].in;
@@ -718,9 +741,13 @@ extern "C" int flrl_fl_compress_rank(flrl_comm *c, const uint8_t *data, size_t s
         ncclComm_t nc = c->dev[0].nccl;
         ncclResult_t r1 = ncclGroupStart();
         if (c->rank == 0) {
-            uint64_t fo = 0, vo = 0;
             for (size_t q = 0; q < R && r1 == ncclSuccess; ++q) {
-                const uint64_t fq = all[2 * q], vq = all[2 * q + 1];
+                // rank q's payload goes to its exchanged offsets (the same
+                // record the device scan gave rank q)
+                uint64_t qr[FLRL_SZ_COUNT];
+                (void)shard_record(all.data(), (uint32_t)R, (uint32_t)R, 1, (uint32_t)q, qr);
+                const uint64_t fq = qr[FLRL_SZ_F], vq = qr[FLRL_SZ_V];
+                const uint64_t fo = qr[FLRL_SZ_F_OFF], vo = qr[FLRL_SZ_V_OFF];
                 if (q == 0) {
                     if ((fq && hipMemcpyAsync(d_all, b.bits, fq, hipMemcpyDeviceToDevice, b.s) != hipSuccess) ||
                         (vq && hipMemcpyAsync(d_all + F, b.vals, vq, hipMemcpyDeviceToDevice, b.s) != hipSuccess))
@@ -731,8 +758,6 @@ extern "C" int flrl_fl_compress_rank(flrl_comm *c, const uint8_t *data, size_t s
                     if (r1 == ncclSuccess && vq)
                         r1 = ncclRecv(d_all + F + vo, vq, ncclUint8, (int)q, nc, b.s);
                 }
-                fo += fq;
-                vo += vq;
             }
         } else {
             if (rec[FLRL_SZ_F])

@@ -33,6 +33,7 @@
 
 #include <atomic>
 #include <condition_variable>
+#include <list>
 #include <map>
 #include <mutex>
 #include <string>
@@ -311,43 +312,69 @@ struct MemFl {  // FL arrays in host memory
 
 // Pinned staging + device buffers of one pipeline, kept across calls: a
 // pipeline's hipHostMalloc/hipMalloc of 2 x ~2 chunks costs more than a
-// 16 MiB chunk's transfer. At most kPoolCap idle sets are kept per shape.
-constexpr size_t kPoolCap = 8;
+// 16 MiB chunk's transfer. Idle sets wait in one pool, most recently used
+// last; past kPoolBytes of idle pinned memory the least recently used sets are
+// freed (a set holds as much HBM as pinned memory), and flrl_release_staging
+// frees every idle set. The host-buffer API's 8 pipelines of 16 MiB chunks
+// hold 512 MiB of pinned memory per direction (compress, decompress).
+constexpr size_t kPoolBytes = 1ull << 30;
 struct PoolKey {
     int dev;
     size_t a, b, c, scr;
-    bool operator<(const PoolKey &o) const
+    bool operator==(const PoolKey &o) const
     {
-        if (dev != o.dev)
-            return dev < o.dev;
-        if (a != o.a)
-            return a < o.a;
-        if (b != o.b)
-            return b < o.b;
-        if (c != o.c)
-            return c < o.c;
-        return scr < o.scr;
+        return dev == o.dev && a == o.a && b == o.b && c == o.c && scr == o.scr;
     }
+    size_t pinned() const { return 2 * (a + b + c + 16); }
+};
+struct PoolEntry {
+    PoolKey key;
+    Slots *x;
 };
 std::mutex g_pool_m;
-std::map<PoolKey, std::vector<Slots *>> g_pool;
+std::list<PoolEntry> g_pool;  // idle sets, least recently used first
+size_t g_pool_bytes = 0;      // their pinned bytes
+
+// Frees `v`'s sets and restores the calling thread's device.
+void free_sets(std::vector<Slots *> &v)
+{
+    if (v.empty())
+        return;
+    int prev = 0;
+    const bool had = hipGetDevice(&prev) == hipSuccess;
+    for (Slots *x : v)
+        delete x;
+    if (had)
+        (void)hipSetDevice(prev);
+    v.clear();
+}
 
 Slots *slots_acquire(int dev, size_t a, size_t b, size_t c, size_t scr)
 {
+    const PoolKey k{dev, a, b, c, scr};
     {
         std::lock_guard<std::mutex> g(g_pool_m);
-        auto it = g_pool.find(PoolKey{dev, a, b, c, scr});
-        if (it != g_pool.end() && !it->second.empty()) {
-            Slots *x = it->second.back();
-            it->second.pop_back();
-            return x;
-        }
+        for (auto it = g_pool.rbegin(); it != g_pool.rend(); ++it)
+            if (it->key == k) {
+                Slots *x = it->x;
+                g_pool_bytes -= k.pinned();
+                g_pool.erase(std::next(it).base());
+                return x;
+            }
     }
     Slots *x = new Slots;
     x->dev = dev;
     if (x->alloc(a, b, c, scr) != hipSuccess) {
         delete x;
-        return nullptr;
+        // an allocation can fail because idle sets hold the memory: free them, retry once
+        if (flrl_release_staging() == 0)
+            return nullptr;
+        x = new Slots;
+        x->dev = dev;
+        if (x->alloc(a, b, c, scr) != hipSuccess) {
+            delete x;
+            return nullptr;
+        }
     }
     return x;
 }
@@ -358,16 +385,44 @@ void slots_release(Slots *x, size_t a, size_t b, size_t c, size_t scr)
         return;
     for (Slot &y : x->slot)  // idle: nothing of a previous call still in flight
         (void)hipStreamSynchronize(y.s);
+    std::vector<Slots *> evict;
     {
         std::lock_guard<std::mutex> g(g_pool_m);
-        std::vector<Slots *> &v = g_pool[PoolKey{x->dev, a, b, c, scr}];
-        if (v.size() < kPoolCap) {
-            v.push_back(x);
-            return;
+        const PoolKey k{x->dev, a, b, c, scr};
+        g_pool.push_back(PoolEntry{k, x});
+        g_pool_bytes += k.pinned();
+        while (g_pool_bytes > kPoolBytes && !g_pool.empty()) {
+            g_pool_bytes -= g_pool.front().key.pinned();
+            evict.push_back(g_pool.front().x);
+            g_pool.pop_front();
         }
     }
-    delete x;
+    free_sets(evict);
 }
+
+}  // namespace
+}  // namespace flrl
+
+extern "C" size_t flrl_release_staging(void)
+{
+    using namespace flrl;
+    std::vector<Slots *> v;
+    size_t freed = 0;
+    {
+        std::lock_guard<std::mutex> g(g_pool_m);
+        for (PoolEntry &e : g_pool) {
+            freed += e.key.pinned();
+            v.push_back(e.x);
+        }
+        g_pool.clear();
+        g_pool_bytes = 0;
+    }
+    free_sets(v);
+    return freed;
+}
+
+namespace flrl {
+namespace {
 
 struct SlotsLease {
     Slots *x = nullptr;
@@ -799,7 +854,7 @@ extern "C" int flrl_fl_compress_file(const char *in_path, const char *out_path, 
     if (::fstat(in.fd, &st) != 0)
         return set_error(FLRL_E_ARG, "[FileIO] Cannot stat file: %s", in_path);
     const uint64_t n = (uint64_t)st.st_size;
-    if (!out.open(out_path))
+    if (!out.open(out_path, false, in.fd))
         return set_error(FLRL_E_ARG, "[FileIO] Cannot open file: %s", out_path);
     const uint64_t F = (n + kFrame - 1) / kFrame;
     FdRaw src{in.fd};
@@ -846,7 +901,7 @@ extern "C" int flrl_fl_decompress_file(const char *in_path, const char *out_path
                          "file %llu bytes)",
                          (unsigned long long)n, (unsigned long long)F, (unsigned long long)V,
                          (unsigned long long)fsize);
-    if (!out.open(out_path))
+    if (!out.open(out_path, false, in.fd))
         return set_error(FLRL_E_ARG, "[FileIO] Cannot open file: %s", out_path);
     if (n == 0 || V == 0) {  // the reference's early-out: empty result (fl_cpu.cu:94-97)
         if (!out.commit())
@@ -974,7 +1029,7 @@ extern "C" int flrl_rl_compress_file(const char *in_path, const char *out_path, 
     if (::fstat(in.fd, &st) != 0)
         return set_error(FLRL_E_ARG, "[FileIO] Cannot stat file: %s", in_path);
     const uint64_t n = (uint64_t)st.st_size;
-    if (!out.open(out_path))
+    if (!out.open(out_path, false, in.fd))
         return set_error(FLRL_E_ARG, "[FileIO] Cannot open file: %s", out_path);
     // values[] until R is known: an anonymous file next to the output
     if ((side.fd = anon_file_near(out_path)) < 0)
@@ -1192,7 +1247,7 @@ extern "C" int flrl_rl_decompress_file(const char *in_path, const char *out_path
             return set_error(FLRL_E_FORMAT, "RL counts sum to %llu, header says %llu",
                              (unsigned long long)out_pos, (unsigned long long)n);
     }
-    if (!out.open(out_path))
+    if (!out.open(out_path, false, in.fd))
         return set_error(FLRL_E_ARG, "[FileIO] Cannot open file: %s", out_path);
     if (!out.truncate(n))
         return set_error(FLRL_E_ARG, "[FileIO] Cannot write to file");

@@ -11,6 +11,8 @@ gpuDecompress, src/fl/fl_gpu.cuh:14-15):
     fl_compress(data) -> FLCompressed(bits, values, input_size)
     fl_decompress(input_size, bits, values) -> np.ndarray[uint8]
     fl_compress_sharded(data, nshards) -> FLCompressed (gpuNCCLCompress, :16)
+Exchange layout (host form of the device scan): shard_range, shard_slot,
+    shard_size_word, shard_scan.
 Multi-GPU (RCCL size exchange; gpuNCCLCompress, fl_gpu.cu:76-287):
     Comm.local(ndev) / Comm.rank(nranks, comm_unique_id(), rank)
     Comm.encode_rank / Comm.compress_rank / Comm.encode_sharded
@@ -97,6 +99,7 @@ _sig("flrl_last_error", ctypes.c_char_p)
 _sig("flrl_version", ctypes.c_char_p)
 _sig("flrl_device_count", ctypes.c_int)
 _sig("flrl_fl_compress", ctypes.c_int, _vp, _sz, ctypes.POINTER(_FLBuf))
+_sig("flrl_release_staging", _sz)
 _sig("flrl_fl_compress_sharded", ctypes.c_int, _vp, _sz, ctypes.c_int, ctypes.POINTER(_FLBuf))
 _sig("flrl_fl_decompress", ctypes.c_int, _sz, _vp, _sz, _vp, _sz,
      ctypes.POINTER(_u8p), ctypes.POINTER(_sz))
@@ -131,6 +134,11 @@ _sig("flrl_comm_query", ctypes.c_int, _vp, ctypes.POINTER(ctypes.c_int),
      ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int))
 _sig("flrl_fl_encode_rank", ctypes.c_int, _vp, _vp, _sz, _vp, _vp, _vp, _vp, _sz, _vp)
 _sig("flrl_fl_compress_rank", ctypes.c_int, _vp, _vp, _sz, ctypes.POINTER(_FLBuf))
+_sig("flrl_shard_range", ctypes.c_int, _sz, ctypes.c_int, ctypes.c_int, ctypes.POINTER(_sz),
+     ctypes.POINTER(_sz))
+_sig("flrl_shard_slot", _sz, ctypes.c_int, ctypes.c_int, ctypes.c_int)
+_sig("flrl_shard_size_word", _u64, _sz)
+_sig("flrl_shard_scan", ctypes.c_int, _vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, _vp)
 _sig("flrl_fl_encode_sharded", ctypes.c_int, _vp, ctypes.c_int, _pp, ctypes.POINTER(_sz), _pp, _pp,
      _pp, _pp, ctypes.POINTER(_sz), _pp)
 
@@ -217,6 +225,41 @@ def fl_compress_sharded(data, nshards: int = 0) -> FLCompressed:
                                          ctypes.byref(buf)))
     return FLCompressed(_take(buf.bits, buf.bits_size), _take(buf.values, buf.values_size),
                         int(buf.input_size))
+
+
+def shard_range(n: int, nshards: int, shard: int) -> tuple[int, int]:
+    """(start, length) of `shard` by the reference rule (file_io.cu:46-51)."""
+    a, b = _sz(), _sz()
+    _check(_lib.flrl_shard_range(n, nshards, shard, ctypes.byref(a), ctypes.byref(b)))
+    return a.value, b.value
+
+
+def shard_slot(shard: int, nshards: int, ndev: int) -> int:
+    """u64 index of shard's {F word, V} pair in the all-gathered exchange array."""
+    s = int(_lib.flrl_shard_slot(shard, nshards, ndev))
+    if s == ctypes.c_size_t(-1).value:
+        raise ValueError(f"shard {shard} of {nshards} on {ndev} devices")
+    return s
+
+
+def shard_size_word(n: int) -> int:
+    """The F word a shard of n bytes puts into its slot (bit 63: ragged)."""
+    return int(_lib.flrl_shard_size_word(n))
+
+
+def shard_scan(gather: np.ndarray, nshards: int, ndev: int, shard: int) -> list[int]:
+    """shard's exchange record [F, V, F_off, V_off, F_total, V_total] from the
+    all-gathered u64 array (the device scan's code); FLRLError(E_ARG) when a
+    shard before the last is ragged."""
+    g = np.ascontiguousarray(gather, dtype=np.uint64)
+    rec = np.zeros(SZ_COUNT, dtype=np.uint64)
+    _check(_lib.flrl_shard_scan(g.ctypes.data, nshards, ndev, shard, rec.ctypes.data))
+    return [int(v) for v in rec]
+
+
+def release_staging() -> int:
+    """Free the host-buffer / file paths' idle pinned staging; returns the bytes."""
+    return int(_lib.flrl_release_staging())
 
 
 def comm_unique_id() -> bytes:

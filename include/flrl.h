@@ -74,6 +74,14 @@ int flrl_device_count(void);             /* number of visible HIP devices (0 if 
  * later calls), so host copies, PCIe transfers and the kernels overlap. */
 int flrl_fl_compress(const uint8_t *data, size_t size, flrl_fl_buf *out);
 
+/* The host-buffer and file paths keep their pinned staging and device buffers
+ * for later calls (per device and chunk shape; after a flrl_fl_compress plus a
+ * flrl_fl_decompress: 1 GiB of pinned host memory and 1 GiB of HBM). Idle sets
+ * are capped at 1 GiB of pinned memory (least recently used freed first) and
+ * freed when an allocation fails; this frees every idle set now and returns
+ * the pinned bytes released (sets in use by running calls are not touched). */
+size_t flrl_release_staging(void);
+
 /* Replaces FixedLength::gpuDecompress (src/fl/fl_gpu.cuh:15, fl_gpu.cu:537-645)
  * and cpuDecompress (src/fl/fl_cpu.cuh:10). Keeps the reference's early-out: if
  * values_size == 0 || bits_size == 0 the result is empty (*out = NULL,
@@ -133,7 +141,9 @@ int flrl_comm_query(const flrl_comm *c, int *nranks, int *rank, int *ndev);
  * rank's shard like flrl_fl_encode_device, then fills d_sizes
  * (u64[FLRL_SZ_COUNT], device) with its sizes, offsets and the totals, all on
  * `stream` with no host synchronisation. Every rank of the comm must call it
- * (collective). The device half of gpuNCCLCompress (fl_gpu.cu:76-143). */
+ * (collective). Shards of ranks 0..nranks-2 must be multiples of 128 bytes:
+ * otherwise every rank's scratch error word reads FLRL_E_ARG after the
+ * exchange. The device half of gpuNCCLCompress (fl_gpu.cu:76-143). */
 int flrl_fl_encode_rank(flrl_comm *c, const uint8_t *d_in, size_t n, uint8_t *d_bits,
                         uint8_t *d_values, uint64_t *d_sizes, void *d_scratch,
                         size_t scratch_bytes, void *stream);
@@ -145,8 +155,28 @@ int flrl_fl_encode_rank(flrl_comm *c, const uint8_t *d_in, size_t n, uint8_t *d_
  * merge (fl_gpu.cu:196-238). Payloads travel ncclSend/ncclRecv to rank 0 only. */
 int flrl_fl_compress_rank(flrl_comm *c, const uint8_t *data, size_t size, flrl_fl_buf *out);
 
+/* The exchange's layout, host-callable (the device scan runs the same code,
+ * csrc/flrl_shard_layout.hpp); for callers that place shards themselves and
+ * for tests.
+ *  flrl_shard_range: shard `shard` of `nshards` of an n-byte input by the
+ *    reference rule (loadFileMpi, file_io.cu:46-51, in size_t): every shard but
+ *    the last is floor(n / (128 nshards)) * 128 bytes.
+ *  flrl_shard_slot: u64 index of shard's {F word, V} pair in the all-gathered
+ *    array when nshards shards run on ndev devices (shard r on device r mod ndev;
+ *    one process per GPU: ndev = nshards); (size_t)-1 for bad arguments.
+ *  flrl_shard_size_word: the F word a shard of n bytes contributes (ceil(n/128),
+ *    bit 63 set when n is not a multiple of 128).
+ *  flrl_shard_scan: shard's record (u64[FLRL_SZ_COUNT]) from the gathered
+ *    array; FLRL_E_ARG if a shard before the last is ragged (the record is
+ *    still written). */
+int flrl_shard_range(size_t n, int nshards, int shard, size_t *start, size_t *length);
+size_t flrl_shard_slot(int shard, int nshards, int ndev);
+uint64_t flrl_shard_size_word(size_t n);
+int flrl_shard_scan(const uint64_t *gather, int nshards, int ndev, int shard, uint64_t *rec);
+
 /* Single-process device-resident sharded encode (flrl_comm_init comm): shard r
- * (d_in[r], n[r]; all but the last a multiple of 128 bytes) with its buffers on
+ * (d_in[r], n[r]; all but the last a multiple of 128 bytes, else FLRL_E_ARG)
+ * with its buffers on
  * device devs[r mod ndev], encoded on streams[r]; after the call every
  * streams[r] is ordered after the exchange, and d_sizes[r] holds shard r's
  * record. At most 64 shards per device. */

@@ -164,3 +164,31 @@ def test_output_mode_follows_umask(cli_path, tmp_path):
 def test_output_to_dev_null(cli_path, tmp_path):
     (tmp_path / "in").write_bytes(b"abc" * 100)
     run(cli_path, "c", "fl-cpu", tmp_path / "in", "/dev/null")
+
+
+def test_existing_output_keeps_mode_and_symlink(cli_path, tmp_path):
+    """Replacing an existing output keeps its mode; a symlinked output's target
+    is replaced and the link stays a link (as fopen "wb" would)."""
+    import os
+    import stat
+    src = tmp_path / "in"
+    a = oracle.gen("lo4", 5000, 2)
+    src.write_bytes(a.tobytes())
+    out = tmp_path / "o.fl"
+    out.write_bytes(b"old")
+    os.chmod(out, 0o600)
+    run(cli_path, "c", "fl-cpu", src, out)
+    assert stat.S_IMODE(out.stat().st_mode) == 0o600
+    assert out.read_bytes() == oracle.fl_file_bytes(a)
+    sub = tmp_path / "sub"
+    sub.mkdir()
+    target = sub / "target.fl"
+    target.write_bytes(b"old")
+    os.chmod(target, 0o640)
+    link = tmp_path / "link.fl"
+    link.symlink_to(target)
+    run(cli_path, "c", "fl-cpu", src, link)
+    assert link.is_symlink() and os.readlink(link) == str(target)
+    assert target.read_bytes() == oracle.fl_file_bytes(a)
+    assert stat.S_IMODE(target.stat().st_mode) == 0o640
+    assert sorted(p.name for p in sub.iterdir()) == ["target.fl"]

@@ -8,7 +8,9 @@ reference fl-cpu's whole-input output (golden BMP sha, 1 GiB u8 sha) byte for
 byte. The per-rank entry (flrl_fl_encode_rank,
 flrl_fl_compress_rank) runs with a one-rank communicator: RCCL refuses two
 ranks on one GPU, so its P > 1 case runs on the driver's 8-GPU node
-(bench.py --gpus N) and in tests/test_dist_gloo.py's CPU restatement.
+(bench.py --gpus N); tests/test_dist_gloo.py runs the exchange's layout code
+(flrl_shard_scan, shared with size_scan_kernel) with 2-4 gloo ranks, and
+tests/test_gpu_configs4.py runs BASELINE configs[4]'s eight 16 GiB shards.
 """
 import hashlib
 import os
@@ -187,6 +189,28 @@ def test_device_sharded_wrong_device_buffers(local_comm):
                                   [s.data_ptr() for s in sh.scr], sh.scr_b,
                                   [int(s.cuda_stream) for s in sh.streams])
     assert e.value.code == flrl.E_ARG
+
+
+def test_device_sharded_rejects_ragged_shard(local_comm):
+    """Every shard but the last must be whole frames (file_io.cu:46-51): a
+    ragged earlier shard would misplace its successors, so it is refused."""
+    from flrl.device import gen
+    n = 1 << 20
+    x = gen("u8", n, 1)
+    sh = Shards(x, n, 3)
+    lens = [sh.len[0] + 5, sh.len[1] - 5, sh.len[2]]
+    with pytest.raises(flrl.FLRLError) as e:
+        local_comm.encode_sharded([x.data_ptr(), x.data_ptr() + lens[0], x.data_ptr() + sh.off[2]], lens,
+                                  [b.data_ptr() for b in sh.bits], [v.data_ptr() for v in sh.vals],
+                                  [s.data_ptr() for s in sh.sizes], [s.data_ptr() for s in sh.scr], sh.scr_b,
+                                  [int(s.cuda_stream) for s in sh.streams])
+    assert e.value.code == flrl.E_ARG
+    sh.len[2] -= 3  # a ragged LAST shard is fine
+    sh.encode(local_comm)
+    rec, bits, vals = sh.place()
+    assert sh.errors() == [0] * 3
+    ref = flrl.fl_compress(x[:n - 3].cpu().numpy())
+    assert np.array_equal(bits.cpu().numpy(), ref.bits) and np.array_equal(vals.cpu().numpy(), ref.values)
 
 
 def test_comm_init_errors():

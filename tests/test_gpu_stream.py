@@ -325,3 +325,22 @@ def test_cli_streamed_error_keeps_existing_output(cli_path, tmp_path):
         assert r.returncode == 2 and "[ERROR]" in r.stderr
         assert out.read_bytes() == b"old"
     assert sorted(p.name for p in tmp_path.iterdir()) == ["bad.fl", "out"]
+
+
+def test_release_staging_frees_idle_sets():
+    """The host API keeps its pinned staging between calls (bounded); releasing
+    it frees the idle sets, and the next call allocates afresh."""
+    import flrl
+    rng = np.random.default_rng(9)
+    a = (rng.integers(0, 256, size=(40 << 20) + 77) >> 3).astype(np.uint8)
+    ref_bits, ref_vals = oracle.fl_compress(a[:1 << 20])
+    flrl.release_staging()
+    c = flrl.fl_compress(a)
+    assert np.array_equal(flrl.fl_decompress(a.size, c.bits, c.values), a)
+    freed = flrl.release_staging()
+    # 8 pipelines x 2 slots of (16 MiB in + 128 KiB bits + 16 MiB values) per direction,
+    # as many pipelines as there are chunks (3 of 16 MiB here)
+    assert freed >= 2 * 3 * 2 * (16 << 20)
+    assert flrl.release_staging() == 0
+    c2 = flrl.fl_compress(a[:1 << 20])
+    assert np.array_equal(c2.bits, ref_bits) and np.array_equal(c2.values, ref_vals)
