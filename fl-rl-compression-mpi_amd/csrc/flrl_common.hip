@@ -73,6 +73,17 @@ hipError_t zero_async(void *p, size_t bytes, hipStream_t s)
     return hipGetLastError();
 }
 
+__global__ void raise_error_kernel(Ctrl *ctrl, uint32_t code)
+{
+    raise_error(ctrl, code);
+}
+
+hipError_t raise_error_async(void *scratch, int code, hipStream_t s)
+{
+    hipLaunchKernelGGL(raise_error_kernel, dim3(1), dim3(1), 0, s, static_cast<Ctrl *>(scratch), (uint32_t)code);
+    return hipGetLastError();
+}
+
 static thread_local int g_skip_resets = 0;
 
 hipError_t scratch_reset(void *p, size_t bytes, hipStream_t s)

@@ -86,18 +86,11 @@ __device__ __forceinline__ uint64_t readlane64(uint64_t v, int l)
 // xor-butterfly shuffles were twelve dependent LDS-crossbar round trips.)
 __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v)
 {
-#ifdef FLRL_SUM_XOR  // A/B builds only
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1)
-        v += __shfl_xor(v, o, kWave);
-    return v;
-#else
     v += dpp64_0<0x111>(v);
     v += dpp64_0<0x112>(v);
     v += dpp64_0<0x114>(v);
     v += dpp64_0<0x118>(v);
     return readlane64(v, 15) + readlane64(v, 31) + readlane64(v, 47) + readlane64(v, 63);
-#endif
 }
 
 // OR across each aligned group of 8 lanes with DPP (no LDS crossbar):

@@ -45,6 +45,7 @@
 #include "flrl.h"
 #include "flrl_device.hpp"
 #include "flrl_internal.hpp"
+#include "flrl_tuning.hpp"
 
 namespace flrl {
 
@@ -147,10 +148,7 @@ __device__ __forceinline__ void stage_packed(uint8_t *s, uint32_t off, uint32_t 
 // done by data wave 0 (scripts/ab_encode.py): lo4 -11 %, zero -3 %, 16 GiB u8
 // -2 %, 1 GiB u8 equal. It also takes the tickets (a data wave would wait for
 // its stores to drain before the atomic returns: 16 GiB u8 -2.9 %).
-// Per-tile timestamp hook for scripts/ubench_fl.hip (no-op in the library).
-#ifndef FLRL_FL_TRACE
-#define FLRL_FL_TRACE(tile, k) ((void)0)
-#endif
+// FLRL_FL_TRACE: per-tile timestamp hook (flrl_tuning.hpp; no-op in the library).
 
 template <int T, int ITEMS>
 __global__ __launch_bounds__(T + kWave, 1) void fl_encode_kernel(

@@ -25,6 +25,10 @@ hipError_t zero_async(void *p, size_t bytes, hipStream_t s);
 // call: zero_async unless flrl_debug_skip_scratch_resets asked this thread to
 // skip it (tests of the kernels' stale-ticket checks).
 hipError_t scratch_reset(void *p, size_t bytes, hipStream_t s);
+// Raise FLRL_E_* `code` in the scratch's error word from stream s (stream
+// ordered, no host sync): errors a device call finds on the host side but
+// reports, like the kernels' own, through flrl_scratch_error.
+hipError_t raise_error_async(void *scratch, int code, hipStream_t s);
 // flrl_debug_fail_chunk: true when the streamed file paths should fail chunk c.
 bool debug_fail_chunk(size_t c);
 

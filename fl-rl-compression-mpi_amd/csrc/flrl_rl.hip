@@ -42,48 +42,16 @@
 #include "flrl.h"
 #include "flrl_device.hpp"
 #include "flrl_internal.hpp"
+#include "flrl_tuning.hpp"
 
-// Timing ablations of rl_encode_wave_kernel (scripts/ubench_rl.hip only; the
-// output is wrong with any of them): 1 no look-back, 2 no record stores, 4 no
-// run staging in the scan pass, 8 no head masks / scans (data only touched).
-#ifndef FLRL_RL_ABL
-#define FLRL_RL_ABL 0
-#endif
-// Per-tile timestamps (scripts/ubench_rl.hip -DTRACE): 0 ticket, 1 all waves
-// scanned, 2 map published, 3 look-back resolved, 4 wave 0 emitted.
-#ifndef FLRL_RL_TRACE
-#define FLRL_RL_TRACE(tile, k) ((void)0)
-#endif
-// Priority of wave 0 while it publishes and looks back (s_setprio; 0: none):
-// it shares its SIMD with the staging passes of up to four other waves.
-#ifndef FLRL_RL_LB_PRIO
-#define FLRL_RL_LB_PRIO 0
-#endif
-// Look-back statistics of one call (trace builds): polls that found an
-// unpublished predecessor, and windows composed.
-#ifndef FLRL_RL_LB_STAT
-#define FLRL_RL_LB_STAT(tile, spins, rounds) ((void)(spins), (void)(rounds))
-#endif
 
 namespace flrl {
 
-#ifndef FLRL_RL_LB
-#define FLRL_RL_LB 64
-#endif
-#ifndef FLRL_RL_THREADS
-#define FLRL_RL_THREADS 256
-#endif
 constexpr int kRlThreads = FLRL_RL_THREADS;         // encode workgroup: 4 waves (LB 64: 94 VGPRs, < 32 KiB LDS, 5 per CU)
 constexpr int kRlLaneBytes = FLRL_RL_LB;            // contiguous bytes per lane (64 or 128)
 constexpr int kRlSub = 32768 / (64 * kRlLaneBytes); // sub-chunks per wave chunk (one look-back per tile)
 constexpr int kRlTileBytes = kRlLaneBytes * kRlThreads * kRlSub;  // 128 KiB: 4 waves x 32 KiB
-#ifndef FLRL_RL_LOOKG
-#define FLRL_RL_LOOKG 1
-#endif
 constexpr int kRlLookG = FLRL_RL_LOOKG;  // look-back granules per lane (window 64 G tiles)
-#ifndef FLRL_RL_STAGE
-#define FLRL_RL_STAGE 15360
-#endif
 constexpr int kRlStageBytes = FLRL_RL_STAGE;  // LDS run staging per workgroup
 
 // Block decode workgroups: 512 threads over 8192-run tiles, 2 per CU, unless the
@@ -93,9 +61,6 @@ constexpr int kRlStageBytes = FLRL_RL_STAGE;  // LDS run staging per workgroup
 // (1..1023 bytes, split) -4 %; all-zero +10 %.
 constexpr int kRdThreads = 256;
 constexpr int kRdThreadsWide = 512;
-#ifndef FLRL_RD_NARROW_MEAN
-#define FLRL_RD_NARROW_MEAN 240
-#endif
 constexpr uint64_t kRdNarrowMean = FLRL_RD_NARROW_MEAN;
 template <int T>
 constexpr int rd_per_cu() { return T == 512 ? 2 : 4; }  // LDS-bound: 59 / 31 KB per workgroup
@@ -439,24 +404,6 @@ struct RlWave {
         for (int c = 0; c < CH; ++c)
             x[c] = *reinterpret_cast<const u32x4 *>(my + ((c ^ sw) * 16));
         const uint32_t mylast = x[CH - 1].w >> 24;
-        if (FLRL_RL_ABL & 8) {
-            uint32_t acc = 0;
-#pragma unroll
-            for (int c = 0; c < CH; ++c)
-                acc ^= x[c].x ^ x[c].y ^ x[c].z ^ x[c].w;
-            L.p0 = p_sub;
-#pragma unroll
-            for (int q = 0; q < CH / 2; ++q)
-                L.nat[q] = q == 0 ? (acc & 1u) : 0u;
-            L.ncnt = acc & 1u;
-            L.fpos = 0;
-            L.lpos = 0;
-            L.vbl = LB;
-            L.lrel = kMapIdent;
-            L.smap = kMapIdent;
-            L.sfirst = acc & 1u ? 0u : kNone;
-            return mylast;
-        }
         const uint32_t up = wave_shr1(mylast);
         L.p0 = lane == 0 ? p_sub : up;
         {
@@ -599,7 +546,7 @@ struct RlWave {
                 first = (uint32_t)s * WB + L.sfirst;
             K += ks;
             rel_in = pm_compose(rel_in, L.smap);
-            if (nst == SUB && indep && !(FLRL_RL_ABL & 4))
+            if (nst == SUB && indep)
                 lane_runs(L, h0, h1, cr, slot);
             hook(s);
         }
@@ -652,7 +599,7 @@ struct RlWave {
     __device__ void emit(const Chunk &C, uint64_t h_in, uint32_t c_in, uint8_t *__restrict__ counts,
                          uint8_t *__restrict__ values, uint64_t *__restrict__ runs_out) const
     {
-        if (C.ns == 0 || (FLRL_RL_ABL & 2))
+        if (C.ns == 0)
             return;
         const uint32_t pre = C.pre();
         {
@@ -775,11 +722,8 @@ struct RlWave {
 // One tile per workgroup (grid = tiles), in ticket order: stage, publish the
 // tile map, ONE look-back by wave 0 while waves 1-3 wait, emit. Three block
 // barriers per tile (ticket, wave maps, state).
-#ifndef FLRL_RL_MINW
-#define FLRL_RL_MINW 1
-#endif
 template <int T, int LB, int SUB>
-__global__ __launch_bounds__(T, FLRL_RL_MINW) void rl_encode_wave_kernel(
+__global__ __launch_bounds__(T) void rl_encode_wave_kernel(
     const uint8_t *__restrict__ in, uint64_t n, uint32_t ntiles, uint8_t *__restrict__ counts,
     uint8_t *__restrict__ values, uint64_t *__restrict__ runs_out, Ctrl *ctrl, uint64_t *status)
 {
@@ -816,19 +760,10 @@ __global__ __launch_bounds__(T, FLRL_RL_MINW) void rl_encode_wave_kernel(
 #pragma unroll
         for (int v = 1; v < W; ++v)
             tmap = sm_compose(tmap, s_map[v]);
-        uint64_t st;
-        if (FLRL_RL_LB_PRIO)
-            __builtin_amdgcn_s_setprio(FLRL_RL_LB_PRIO);
-        if (FLRL_RL_ABL & 1) {
-            st = sm_const((uint64_t)tile * 4096u, 0);
-        } else {
-            publish_seg(status, tile, tmap);
-            FLRL_RL_TRACE(tile, 2);
-            st = lookback_seg<kRlLookG>(status, tile, tmap, ctrl);
-            FLRL_RL_TRACE(tile, 3);
-        }
-        if (FLRL_RL_LB_PRIO)
-            __builtin_amdgcn_s_setprio(0);
+        publish_seg(status, tile, tmap);
+        FLRL_RL_TRACE(tile, 2);
+        uint64_t st = lookback_seg<kRlLookG>(status, tile, tmap, ctrl);
+        FLRL_RL_TRACE(tile, 3);
         if (V.lane == 0) {
 #pragma unroll
             for (int v = 0; v < W; ++v) {
@@ -1070,9 +1005,6 @@ constexpr int kRoWaves = kRoThreads / kWave;
 constexpr int kRoQ = 16;                                // count vectors per lane per step
 constexpr int kRoStep = kRoQ * 16 * kWave;              // counts per wave step (16384)
 constexpr int kRoRuns = kRoStep * kRoWaves;             // counts per workgroup and iteration
-#ifndef FLRL_RL_RO_MAXB
-#define FLRL_RL_RO_MAXB 256
-#endif
 constexpr size_t kRoMaxBlocks = FLRL_RL_RO_MAXB;        // workgroups: 256 (1 GiB runs32 call -2 %; 128: random bytes +13 %; 1024: the old cap)
 static_assert(kRoMaxBlocks <= kMaxPrefixBlocks, "block_prefix_all bound");
 
@@ -1445,9 +1377,6 @@ __global__ __launch_bounds__(T) void rl_decode_kernel(
                 const uint32_t wl = ce < (uint32_t)kRkWindow ? ce : (uint32_t)kRkWindow;
                 const uint32_t b0 = tb > 0 ? (uint32_t)tb : 0u;
                 uint8_t *const outw = out + gw;
-#ifndef FLRL_RD_UNROLL  // 8 (a 512-thread window in full): runs32 -3 %, runs of 1..32 -4 % vs 4
-#define FLRL_RD_UNROLL 8
-#endif
 #pragma unroll FLRL_RD_UNROLL
                 for (int k = 0; k < CPT; ++k) {
                     const uint32_t q = (uint32_t)(k * T + tid);
@@ -1539,9 +1468,6 @@ __global__ __launch_bounds__(T) void rl_decode_kernel(
 // longer: +2..4 %, so only the densest inputs take it).
 constexpr int kWdRpl = 32;
 constexpr int kWdRuns = kWave * kWdRpl;    // runs per wave tile (the finest tile_base granularity)
-#ifndef FLRL_RL_WD64_MEAN
-#define FLRL_RL_WD64_MEAN 2
-#endif
 constexpr uint64_t kWd64Mean = FLRL_RL_WD64_MEAN;
 constexpr int kWdWin = 8192;               // output bytes per window
 constexpr int kWdWords = kWdWin / 32;      // bitmap words per window (4 per lane)
@@ -1552,9 +1478,6 @@ constexpr int wd_per_cu() { return RPL == 64 ? 4 : 6; }
 // inputs with a mean run of at most this many bytes take the wave decode
 // (against the 512-thread block decode, 1 GiB: runs of 1..16 -15 %, 1..24
 // equal, 1..32 +4 %)
-#ifndef FLRL_RL_DENSE_MEAN
-#define FLRL_RL_DENSE_MEAN 12
-#endif
 constexpr uint64_t kWdDenseMean = FLRL_RL_DENSE_MEAN;
 static_assert(kWdWords == 4 * kWave, "one bitmap vector per lane");
 
@@ -1886,12 +1809,8 @@ extern "C" int flrl_rl_decode_device(const uint8_t *d_counts, const uint8_t *d_v
         return set_error(FLRL_E_ARG, "flrl_rl_decode_device: scratch not 16-byte aligned");
     FLRL_HIP(scratch_reset(d_scratch, L.zero, s));
     if (runs == 0) {
-        if (n != 0) {
-            const uint32_t e = FLRL_E_FORMAT;
-            FLRL_HIP(hipMemcpyAsync(static_cast<uint8_t *>(d_scratch) + 4, &e, 4,
-                                    hipMemcpyHostToDevice, s));
-            FLRL_HIP(hipStreamSynchronize(s));
-        }
+        if (n != 0)  // no runs cannot make n bytes: flagged like a malformed count
+            FLRL_HIP(raise_error_async(d_scratch, FLRL_E_FORMAT, s));
         return FLRL_OK;
     }
     if (!d_counts || !d_values || !d_out)

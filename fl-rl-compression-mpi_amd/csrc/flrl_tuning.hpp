@@ -1,0 +1,74 @@
+// flrl_tuning.hpp — the kernel shape constants, and the ONLY place where
+// timing harnesses may override them or hook traces into the kernels.
+//
+// The shipped build (Makefile) defines none of the FLRL_* macros below: every
+// constant then takes the value measured best (DESIGN.md §4 records the
+// measurements). The A/B and trace harnesses under scripts/ (build_variant.sh,
+// ubench_*.hip) define FLRL_TUNING_BUILD together with their overrides; an
+// override without it is a compile error, so a stray -D cannot change a
+// shipped library silently.
+#pragma once
+
+#if !defined(FLRL_TUNING_BUILD) &&                                                                  \
+    (defined(FLRL_RL_TRACE) || defined(FLRL_RL_LB_STAT) || defined(FLRL_FL_TRACE) ||                \
+     defined(FLRL_RL_LB) || defined(FLRL_RL_THREADS) || defined(FLRL_RL_LOOKG) ||                   \
+     defined(FLRL_RL_STAGE) || defined(FLRL_RD_NARROW_MEAN) || defined(FLRL_RL_RO_MAXB) ||          \
+     defined(FLRL_RD_UNROLL) || defined(FLRL_RL_WD64_MEAN) || defined(FLRL_RL_DENSE_MEAN))
+#error "FLRL_* kernel overrides are for timing harnesses only (define FLRL_TUNING_BUILD)"
+#endif
+
+// ---- trace hooks (no-ops unless a harness supplies them) -------------------
+// FL encode per-tile timestamps (scripts/ubench_fl.hip -DTRACE): 0 ticket,
+// 1 widths done, 2 look-back resolved, 3 stores issued.
+#ifndef FLRL_FL_TRACE
+#define FLRL_FL_TRACE(tile, k) ((void)0)
+#endif
+// RL encode per-tile timestamps (scripts/ubench_rl.hip -DTRACE): 0 ticket,
+// 1 all waves scanned, 2 map published, 3 look-back resolved, 4 wave 0 emitted.
+#ifndef FLRL_RL_TRACE
+#define FLRL_RL_TRACE(tile, k) ((void)0)
+#endif
+// RL encode look-back statistics: polls that found an unpublished
+// predecessor, and windows composed.
+#ifndef FLRL_RL_LB_STAT
+#define FLRL_RL_LB_STAT(tile, spins, rounds) ((void)(spins), (void)(rounds))
+#endif
+
+// ---- RL encode shape ---------------------------------------------------------
+#ifndef FLRL_RL_LB
+#define FLRL_RL_LB 64  // contiguous bytes per lane (64 or 128)
+#endif
+#ifndef FLRL_RL_THREADS
+#define FLRL_RL_THREADS 256  // 4 waves (LB 64: 94 VGPRs, < 32 KiB LDS, 5 per CU)
+#endif
+#ifndef FLRL_RL_LOOKG
+#define FLRL_RL_LOOKG 1  // look-back granules per lane (window 64 G tiles)
+#endif
+#ifndef FLRL_RL_STAGE
+#define FLRL_RL_STAGE 15360  // LDS run staging per workgroup (bytes)
+#endif
+
+// ---- RL decode shape ---------------------------------------------------------
+// Block decode: 256 instead of 512 threads per workgroup from this mean run
+// length (bytes) on.
+#ifndef FLRL_RD_NARROW_MEAN
+#define FLRL_RD_NARROW_MEAN 240
+#endif
+// Offsets pre-pass workgroups: 256 (1 GiB runs32 call -2 %; 128: random bytes
+// +13 %; 1024: the old cap).
+#ifndef FLRL_RL_RO_MAXB
+#define FLRL_RL_RO_MAXB 256
+#endif
+// Block decode chunk loop unroll: 8 (a 512-thread window in full): runs32
+// -3 %, runs of 1..32 -4 % vs 4.
+#ifndef FLRL_RD_UNROLL
+#define FLRL_RD_UNROLL 8
+#endif
+// Wave decode: 64 runs per lane up to this mean run length, and the wave
+// decode at all up to FLRL_RL_DENSE_MEAN.
+#ifndef FLRL_RL_WD64_MEAN
+#define FLRL_RL_WD64_MEAN 2
+#endif
+#ifndef FLRL_RL_DENSE_MEAN
+#define FLRL_RL_DENSE_MEAN 12
+#endif

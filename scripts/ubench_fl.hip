@@ -11,6 +11,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#define FLRL_TUNING_BUILD 1  // trace hooks below (csrc/flrl_tuning.hpp)
+
 #ifdef TRACE
 __device__ uint64_t *g_trace;
 __device__ __forceinline__ uint64_t fl_rtime()

@@ -9,6 +9,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#define FLRL_TUNING_BUILD 1  // trace hooks below (csrc/flrl_tuning.hpp)
+
 __device__ unsigned long long g_ph[64];
 __device__ __forceinline__ uint64_t rl_stamp()
 {
