@@ -273,10 +273,10 @@ def north_star_section(seed: int, steps: int, warmup: int, dev):
     return res
 
 
-def _rl_timed(x, n: int, steps: int, warmup: int, dev):
+def _rl_timed(x, n: int, steps: int, warmup: int, dev, form: int = flrl.RL_FORM_LOOKBACK):
     """RL encode + decode of x (n bytes in HBM): R, the round trip, and mean
     whole-call / kernel-alone times of both (HIP events)."""
-    d = RLDevice(n, dev)
+    d = RLDevice(n, dev, form)
     stream = torch.cuda.current_stream()
     d.encode(x)
     R = d.runs()
@@ -302,9 +302,9 @@ def _rl_timed(x, n: int, steps: int, warmup: int, dev):
     return d, R, ok, t
 
 
-def _rl_encode_alone(x, n: int, steps: int, warmup: int, dev):
+def _rl_encode_alone(x, n: int, steps: int, warmup: int, dev, form: int = flrl.RL_FORM_LOOKBACK):
     """mean kernel ms of back-to-back RL encodes of x (no decode between)"""
-    d = RLDevice(n, dev)
+    d = RLDevice(n, dev, form)
     stream = torch.cuda.current_stream()
     for _ in range(warmup + 1):
         d.encode(x)
@@ -320,24 +320,17 @@ def _rl_encode_alone(x, n: int, steps: int, warmup: int, dev):
 
 
 def rl_encode_forms(x, n: int, R: int, steps: int, warmup: int, dev):
-    """Kernel ms of both RL encode forms (FLRL_RL_ENCODE_PASSES 1 = default,
-    3 = scan/state/emit) in the encode/decode loop and encoding alone: the
-    three-pass form wins alone and loses in the loop."""
+    """Kernel ms of both RL encode forms (the C-ABI form argument: 1 = the
+    look-back pass, the default; 3 = scan/state/emit) in the encode/decode
+    loop and encoding alone: the three-pass form wins alone and loses in the
+    loop."""
     res = {}
-    old = os.environ.get("FLRL_RL_ENCODE_PASSES")
-    try:
-        for p in ("1", "3"):
-            os.environ["FLRL_RL_ENCODE_PASSES"] = p
-            d, R2, ok, (_, _, enc_k, _) = _rl_timed(x, n, steps, warmup, dev)
-            del d
-            alone = _rl_encode_alone(x, n, steps, warmup, dev)
-            res[p] = {"loop_ms": round(enc_k, 4), "alone_ms": round(alone, 4), "roundtrip": ok and R2 == R}
-            torch.cuda.empty_cache()
-    finally:
-        if old is None:
-            os.environ.pop("FLRL_RL_ENCODE_PASSES", None)
-        else:
-            os.environ["FLRL_RL_ENCODE_PASSES"] = old
+    for form in (flrl.RL_FORM_LOOKBACK, flrl.RL_FORM_THREE_PASS):
+        d, R2, ok, (_, _, enc_k, _) = _rl_timed(x, n, steps, warmup, dev, form)
+        del d
+        alone = _rl_encode_alone(x, n, steps, warmup, dev, form)
+        res[str(form)] = {"loop_ms": round(enc_k, 4), "alone_ms": round(alone, 4), "roundtrip": ok and R2 == R}
+        torch.cuda.empty_cache()
     return res
 
 

@@ -1670,19 +1670,6 @@ __global__ __launch_bounds__(kWdThreads) void rl_decode_wave_kernel(
     }
 }
 
-// Encode passes: 1 (default) or 3, chosen per call by the environment
-// variable FLRL_RL_ENCODE_PASSES (read when the scratch is sized and when the
-// encode is launched, so set it before both). The three-pass form is 15 %
-// faster on runs32 when the input follows other reads, equal when it follows
-// 1 GiB of writes (their dirty lines are written back during its scan pass, which
-// is bandwidth-bound where the single pass waits in look-backs), and 9 % slower
-// inside bench.py's encode/decode loop.
-static bool rl_three_pass()
-{
-    const char *e = getenv("FLRL_RL_ENCODE_PASSES");
-    return e && e[0] == '3';
-}
-
 // single pass: [Ctrl][status: tiles] (zeroed); three passes: [Ctrl] (zeroed)
 // [tmap: tiles][tlocal: tiles][bagg: blocks x 32 B][bpre: blocks x 16 B]
 // [sums: tiles x 4 x 48 B][staged runs: tiles x kRlStageBytes]
@@ -1734,15 +1721,31 @@ struct RlDecLayout {
 
 using namespace flrl;
 
-extern "C" size_t flrl_rl_scratch_bytes(size_t n) { return RlEncLayout(n, rl_three_pass()).bytes; }
+static bool rl_form_known(int form) { return form == FLRL_RL_FORM_LOOKBACK || form == FLRL_RL_FORM_THREE_PASS; }
+
+extern "C" size_t flrl_rl_scratch_bytes_form(size_t n, int form)
+{
+    return rl_form_known(form) ? RlEncLayout(n, form == FLRL_RL_FORM_THREE_PASS).bytes : 0;
+}
+extern "C" size_t flrl_rl_scratch_bytes(size_t n) { return flrl_rl_scratch_bytes_form(n, FLRL_RL_FORM_LOOKBACK); }
 extern "C" size_t flrl_rl_decode_scratch_bytes(size_t runs) { return RlDecLayout(runs).bytes; }
 
 extern "C" int flrl_rl_encode_device(const uint8_t *d_in, size_t n, uint8_t *d_counts,
                                      uint8_t *d_values, uint64_t *d_runs, void *d_scratch,
                                      size_t scratch_bytes, void *stream)
 {
+    return flrl_rl_encode_device_form(d_in, n, d_counts, d_values, d_runs, d_scratch, scratch_bytes, stream,
+                                      FLRL_RL_FORM_LOOKBACK);
+}
+
+extern "C" int flrl_rl_encode_device_form(const uint8_t *d_in, size_t n, uint8_t *d_counts,
+                                          uint8_t *d_values, uint64_t *d_runs, void *d_scratch,
+                                          size_t scratch_bytes, void *stream, int form)
+{
     hipStream_t s = static_cast<hipStream_t>(stream);
-    const bool three = rl_three_pass();
+    if (!rl_form_known(form))
+        return set_error(FLRL_E_ARG, "flrl_rl_encode_device_form: unknown form %d", form);
+    const bool three = form == FLRL_RL_FORM_THREE_PASS;
     const RlEncLayout L(n, three);
     if (!d_runs || !d_scratch)
         return set_error(FLRL_E_ARG, "flrl_rl_encode_device: null runs/scratch");

@@ -102,17 +102,31 @@ def test_scratch_sizes_monotone():
         assert sizes == sorted(sizes), f.__name__
 
 
-@pytest.mark.parametrize("passes", ["1", "3"])
-def test_rl_encode_scratch_per_form(passes, monkeypatch):
-    # FLRL_RL_ENCODE_PASSES picks the encode form when the scratch is sized:
-    # the three-pass form stages runs in the scratch (about 12 % of n), the
-    # single pass needs only its tile states; both grow with n
-    monkeypatch.setenv("FLRL_RL_ENCODE_PASSES", passes)
+@pytest.mark.parametrize("form", [flrl.RL_FORM_LOOKBACK, flrl.RL_FORM_THREE_PASS])
+def test_rl_encode_scratch_per_form(form):
+    # the encode form is an explicit argument of the sizing (a pure function of
+    # (n, form)): the three-pass form stages runs in the scratch (about 12 % of
+    # n), the single pass needs only its tile states; both grow with n
     pts = [1, 4096, 131072, 131073, 10 ** 6, 1 << 30]
-    sizes = [flrl.rl_scratch_bytes(x) for x in pts]
+    sizes = [flrl.rl_scratch_bytes(x, form) for x in pts]
     assert sizes == sorted(sizes)
-    big = flrl.rl_scratch_bytes(1 << 30)
-    if passes == "3":
+    big = flrl.rl_scratch_bytes(1 << 30, form)
+    if form == flrl.RL_FORM_THREE_PASS:
         assert (1 << 30) // 10 < big < (1 << 30) // 5
     else:
         assert big < (1 << 30) // 100
+        assert big == flrl.rl_scratch_bytes(1 << 30) == flrl.lib_handle().flrl_rl_scratch_bytes(1 << 30)
+
+
+def test_rl_encode_form_ignores_environment(monkeypatch):
+    # the round-2 environment switch is gone: sizing does not read it
+    before = flrl.rl_scratch_bytes(1 << 30)
+    monkeypatch.setenv("FLRL_RL_ENCODE_PASSES", "3")
+    assert flrl.rl_scratch_bytes(1 << 30) == before
+
+
+def test_rl_encode_unknown_form():
+    assert flrl.rl_scratch_bytes(1 << 20, 2) == 0
+    # rejected before any device work (no GPU needed)
+    rc = flrl.lib_handle().flrl_rl_encode_device_form(None, 0, None, None, None, None, 0, None, 2)
+    assert rc == flrl.E_ARG

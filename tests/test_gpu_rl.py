@@ -25,33 +25,59 @@ def _need_gpu():
         pytest.fail("GPU tests need a HIP device")
 
 
-@pytest.fixture(params=["1", "3"])
-def passes(request, monkeypatch):
-    """Encode tests run with both encode forms: the single look-back pass
-    (default) and the scan/state/emit passes (FLRL_RL_ENCODE_PASSES=3)."""
-    monkeypatch.setenv("FLRL_RL_ENCODE_PASSES", request.param)
+@pytest.fixture(params=[flrl.RL_FORM_LOOKBACK, flrl.RL_FORM_THREE_PASS], ids=["lookback", "3pass"])
+def passes(request):
+    """Encode tests run with both encode forms (an explicit C-ABI argument):
+    the single look-back pass (the default, reached through the host API
+    flrl_rl_compress) and the scan/state/emit passes (flrl_rl_encode_device_form)."""
     return request.param
 
 
+FORM = flrl.RL_FORM_LOOKBACK  # the form check() encodes with; set per test by _form
+
+
+@pytest.fixture(autouse=True)
+def _form(request):
+    global FORM
+    FORM = request.getfixturevalue("passes") if "passes" in request.fixturenames else flrl.RL_FORM_LOOKBACK
+    yield
+    FORM = flrl.RL_FORM_LOOKBACK
+
+
+def encode(a: np.ndarray, form: int):
+    """RL records of `a` from the encode form under test: the host API for the
+    default form, the device API with the form argument otherwise."""
+    if form == flrl.RL_FORM_LOOKBACK:
+        r = flrl.rl_compress(a)
+        assert r.input_size == a.size
+        return r.counts, r.values
+    from flrl.device import RLDevice
+    d = RLDevice(a.size, form=form)
+    x = torch.from_numpy(np.ascontiguousarray(a)).cuda()
+    d.encode(x)
+    R = d.runs()
+    assert d.error() == 0
+    return d.counts[:R].cpu().numpy(), d.values[:R].cpu().numpy()
+
+
 def check(a: np.ndarray):
-    r = flrl.rl_compress(a)
+    rc, rv = encode(a, FORM)
     counts, values = oracle.rl_compress(a)
-    assert r.input_size == a.size
-    assert r.counts.size == counts.size, (r.counts.size, counts.size)
-    assert np.array_equal(r.counts, counts)
-    assert np.array_equal(r.values, values)
-    back = flrl.rl_decompress(a.size, r.counts, r.values)
+    assert rc.size == counts.size, (rc.size, counts.size)
+    assert np.array_equal(rc, counts)
+    assert np.array_equal(rv, values)
+    back = flrl.rl_decompress(a.size, rc, rv)
     assert np.array_equal(back, a)
-    return r
+    return flrl.RLCompressed(rc, rv, a.size)
 
 
 def test_kats(golden, passes):
     for case in golden["rl_kat"]:
         data = np.frombuffer(kat_input(case), np.uint8)
-        r = flrl.rl_compress(data)
-        assert r.counts.tolist() == case["counts"], case["name"]
-        assert r.values.tolist() == case["values"], case["name"]
-        assert flrl.rl_decompress(data.size, r.counts, r.values).tobytes() == data.tobytes()
+        c, v = encode(data, passes)
+        assert c.tolist() == case["counts"], case["name"]
+        assert v.tolist() == case["values"], case["name"]
+        assert flrl.rl_decompress(data.size, c, v).tobytes() == data.tobytes()
 
 
 def test_empty():
@@ -151,7 +177,7 @@ def test_device_1gib_runs32(passes):
     a = oracle.gen("runs32", n, 42)
     counts, values = oracle.rl_compress(a)
     x = torch.from_numpy(a).cuda()
-    d = RLDevice(n)
+    d = RLDevice(n, form=passes)
     d.encode(x)
     R = d.runs()
     assert d.error() == 0
@@ -254,7 +280,7 @@ def test_device_more_than_2_32_runs(passes):
     from flrl.device import RLDevice, gen
     n = (1 << 32) + (1 << 28) + 12345
     x = gen("u8", n, 77)
-    d = RLDevice(n)
+    d = RLDevice(n, form=passes)
     d.encode(x)
     R = d.runs()
     assert d.error() == 0
