@@ -1173,6 +1173,52 @@ __device__ __forceinline__ void store_chunk_part(uint8_t *dst, u32x4 v, uint32_t
         dst[a] = (uint8_t)(dw(a) >> (8 * (a & 3)));
 }
 
+// One 16-byte output chunk of a rank-decode window (block and wave decode):
+// q = the chunk's index in the window; bm / pre = the window's start bitmap
+// and the runs starting before each bitmap word; v32 = the tile's values (run
+// indices tile-local); pfx = the byte-prefix popcount table; before = runs
+// starting before the window. The run of the chunk's first byte is (runs
+// before it) + (its start bit) - 1; byte i takes run r + k_i (k_i = start bits
+// in bytes 1..i, <= 15), gathered from the 16 values from run r on with byte
+// permutes.
+__device__ __forceinline__ u32x4 rd_chunk(const uint32_t *bm, const uint32_t *pre, const uint32_t *v32,
+                                          const uint64_t *pfx, uint32_t q, uint32_t before)
+{
+    const uint32_t word = bm[q >> 1];
+    const uint32_t m = (q & 1) ? word >> 16 : word & 0xFFFFu;
+    const uint32_t pq = pre[q >> 1] + ((q & 1) ? __popc(word & 0xFFFFu) : 0u);
+    int32_t r = (int32_t)(before + pq + (m & 1u)) - 1;  // run of byte 0
+    uint32_t m1 = m & 0xFFFEu;                            // starts after byte 0
+    if (r < 0) {  // bytes before the tile's first start are not stored
+        m1 &= m1 - 1;
+        r = 0;
+    }
+    // (no separate path for chunks without an inner start, m1 = 0: a wave
+    // almost always holds both kinds, so it would run both; -2 %)
+    const uint32_t a = (uint32_t)r >> 2, sh = (uint32_t)r & 3u;
+    const uint32_t d0 = v32[a], d1 = v32[a + 1], d2 = v32[a + 2], d3 = v32[a + 3], d4 = v32[a + 4];
+    const uint32_t w0 = __builtin_amdgcn_alignbyte(d1, d0, sh);
+    const uint32_t w1 = __builtin_amdgcn_alignbyte(d2, d1, sh);
+    const uint32_t w2 = __builtin_amdgcn_alignbyte(d3, d2, sh);
+    const uint32_t w3 = __builtin_amdgcn_alignbyte(d4, d3, sh);
+    // k_i as bytes: pfx[x] byte i = popcount of x's bits 0..i (a table: no
+    // 64-bit multiplies); the high half adds the low byte's total (no
+    // multiplies: v_mul_lo_u32 is a quarter-rate instruction)
+    const uint64_t klo = pfx[m1 & 0xFFu], kh = pfx[m1 >> 8];
+    const uint32_t plo = __builtin_amdgcn_perm(0u, (uint32_t)__popc(m1 & 0xFFu), 0u);
+    const uint32_t k4[4] = {(uint32_t)klo, (uint32_t)(klo >> 32), (uint32_t)kh + plo, (uint32_t)(kh >> 32) + plo};
+    u32x4 o;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+        const uint32_t sel = k4[d];
+        const uint32_t lo8 = __builtin_amdgcn_perm(w1, w0, sel & 0x07070707u);
+        const uint32_t hi8 = __builtin_amdgcn_perm(w3, w2, sel & 0x07070707u);
+        // byte i from hi8 (selector 4 + i) where k_i >= 8, else from lo8 (i)
+        o[d] = __builtin_amdgcn_perm(hi8, lo8, ((sel >> 1) & 0x04040404u) | 0x03020100u);
+    }
+    return o;
+}
+
 // ---- decode by rank: output-driven windows ---------------------------------
 // Every lane produces whole 16-byte output chunks, stored coalesced straight
 // from registers. Per kRkWindow-byte window of a tile's output: (1) each run
@@ -1206,7 +1252,9 @@ __global__ __launch_bounds__(T) void rl_decode_kernel(
     constexpr int CPT = kRkWindow / 16 / T; // chunks per thread per window
     static_assert(RPT == 16 && WPT % 4 == 0, "one 16-byte count/value vector, whole bitmap vectors per thread");
     // [bitmap: kRkWords][s_pre: kRkWords][s_st: kRdRuns + 1] u32; a dense tile
-    // (output <= kRkDense bytes) uses the same LDS as its byte output window
+    // (output <= kRkDense bytes) uses the same LDS as its byte output window.
+    // (Two bitmaps alternating by window, three barriers per window instead of
+    // five: no change on any input kind)
     __shared__ u32x4 s_big4[(2 * kRkWords + kRdRuns + 1 + 3) / 4];
     __shared__ u32x4 s_val4[kRdRuns / 16 + 1];  // +16 B: the permute window reads up to 19 bytes past a run
     __shared__ uint32_t s_wave[T / kWave];
@@ -1383,45 +1431,8 @@ __global__ __launch_bounds__(T) void rl_decode_kernel(
                     const uint32_t off = 16u * q;
                     if (off >= wl)
                         break;
-                    const uint32_t word = s_bm[q >> 1];
-                    const uint32_t m = (q & 1) ? word >> 16 : word & 0xFFFFu;
-                    const uint32_t pre = s_pre[q >> 1] + ((q & 1) ? __popc(word & 0xFFFFu) : 0u);
-                    int32_t r = (int32_t)(starts_before + pre + (m & 1u)) - 1;  // run of byte 0
-                    uint32_t m1 = m & 0xFFFEu;  // starts after byte 0
-                    if (r < 0) {  // bytes before the tile's first start are not stored
-                        m1 &= m1 - 1;
-                        r = 0;
-                    }
-                    // (no separate path for chunks without an inner start, m1 = 0: a wave
-                    // almost always holds both kinds, so it would run both; -2 %)
-                    u32x4 o;
-                    {
-                        // byte i takes run r + k_i, k_i = starts in bytes 1..i (<= 15): the
-                        // 16 values from run r on are gathered with byte permutes
-                        const uint32_t *v32 = reinterpret_cast<const uint32_t *>(s_val4);
-                        const uint32_t a = (uint32_t)r >> 2, sh = (uint32_t)r & 3u;
-                        const uint32_t d0 = v32[a], d1 = v32[a + 1], d2 = v32[a + 2], d3 = v32[a + 3],
-                                       d4 = v32[a + 4];
-                        const uint32_t w0 = __builtin_amdgcn_alignbyte(d1, d0, sh);
-                        const uint32_t w1 = __builtin_amdgcn_alignbyte(d2, d1, sh);
-                        const uint32_t w2 = __builtin_amdgcn_alignbyte(d3, d2, sh);
-                        const uint32_t w3 = __builtin_amdgcn_alignbyte(d4, d3, sh);
-                        // k_i as bytes: s_pfx[x] byte i = popcount of x's bits 0..i (a table:
-                        // no 64-bit multiplies); the high half adds the low byte's total
-                        // (no multiplies: v_mul_lo_u32 is a quarter-rate instruction)
-                        const uint64_t klo = s_pfx[m1 & 0xFFu], kh = s_pfx[m1 >> 8];
-                        const uint32_t plo = __builtin_amdgcn_perm(0u, (uint32_t)__popc(m1 & 0xFFu), 0u);
-                        const uint32_t k4[4] = {(uint32_t)klo, (uint32_t)(klo >> 32), (uint32_t)kh + plo,
-                                                (uint32_t)(kh >> 32) + plo};
-#pragma unroll
-                        for (int d = 0; d < 4; ++d) {
-                            const uint32_t sel = k4[d];
-                            const uint32_t lo8 = __builtin_amdgcn_perm(w1, w0, sel & 0x07070707u);
-                            const uint32_t hi8 = __builtin_amdgcn_perm(w3, w2, sel & 0x07070707u);
-                            // byte i from hi8 (selector 4 + i) where k_i >= 8, else from lo8 (i)
-                            o[d] = __builtin_amdgcn_perm(hi8, lo8, ((sel >> 1) & 0x04040404u) | 0x03020100u);
-                        }
-                    }
+                    const u32x4 o = rd_chunk(s_bm, s_pre, reinterpret_cast<const uint32_t *>(s_val4), s_pfx, q,
+                                             starts_before);
                     if (off >= b0 && off + 16 <= ce) {
                         *reinterpret_cast<u32x4 *>(outw + off) = o;  // plain: see the note above
                     } else {  // a chunk shared with a neighbouring tile: its bytes only
@@ -1619,39 +1630,7 @@ __global__ __launch_bounds__(kWdThreads) void rl_decode_wave_kernel(
                 const uint32_t nch = (wl + 15) / 16;
                 for (uint32_t q = lane; q < nch; q += kWave) {  // (unrolled by 2 or 4: +1..7 %)
                     const uint32_t gq = w + 16u * q;  // window-relative chunk start
-                    const uint32_t word = bm[q >> 1];
-                    const uint32_t m = (q & 1) ? word >> 16 : word & 0xFFFFu;
-                    const uint32_t pq = pre[q >> 1] + ((q & 1) ? __popc(word & 0xFFFFu) : 0u);
-                    int32_t r = (int32_t)(starts_before + pq + (m & 1u)) - 1;  // run of byte 0
-                    uint32_t m1 = m & 0xFFFEu;  // starts after byte 0
-                    if (r < 0) {  // bytes before the tile's first start are not stored
-                        m1 &= m1 - 1;
-                        r = 0;
-                    }
-                    u32x4 ov;
-                    {  // (every chunk takes the permute path, as in the block decode)
-                        // byte i takes run r + k_i, k_i = starts in bytes 1..i (<= 15)
-                        const uint32_t a = (uint32_t)r >> 2, sh = (uint32_t)r & 3u;
-                        const uint32_t d0 = sv32[a], d1 = sv32[a + 1], d2 = sv32[a + 2], d3 = sv32[a + 3],
-                                       d4 = sv32[a + 4];
-                        const uint32_t w0 = __builtin_amdgcn_alignbyte(d1, d0, sh);
-                        const uint32_t w1 = __builtin_amdgcn_alignbyte(d2, d1, sh);
-                        const uint32_t w2 = __builtin_amdgcn_alignbyte(d3, d2, sh);
-                        const uint32_t w3 = __builtin_amdgcn_alignbyte(d4, d3, sh);
-                        // (no multiplies: v_mul_lo_u32 is a quarter-rate instruction)
-                        const uint64_t klo = s_pfx[m1 & 0xFFu], kh = s_pfx[m1 >> 8];
-                        const uint32_t plo = __builtin_amdgcn_perm(0u, (uint32_t)__popc(m1 & 0xFFu), 0u);
-                        const uint32_t k4[4] = {(uint32_t)klo, (uint32_t)(klo >> 32), (uint32_t)kh + plo,
-                                                (uint32_t)(kh >> 32) + plo};
-#pragma unroll
-                        for (int d = 0; d < 4; ++d) {
-                            const uint32_t sel = k4[d];
-                            const uint32_t lo8 = __builtin_amdgcn_perm(w1, w0, sel & 0x07070707u);
-                            const uint32_t hi8 = __builtin_amdgcn_perm(w3, w2, sel & 0x07070707u);
-                            // byte i from hi8 (selector 4 + i) where k_i >= 8, else from lo8 (i)
-                            ov[d] = __builtin_amdgcn_perm(hi8, lo8, ((sel >> 1) & 0x04040404u) | 0x03020100u);
-                        }
-                    }
+                    const u32x4 ov = rd_chunk(bm, pre, sv32, s_pfx, q, starts_before);
                     const uint32_t b0 = (uint32_t)(base - g0);
                     const uint32_t lo = gq < b0 ? b0 - gq : 0u;
                     const uint32_t hi = gq + 16 > len ? len - gq : 16u;

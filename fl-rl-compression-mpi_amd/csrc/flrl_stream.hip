@@ -42,6 +42,7 @@
 
 #include "flrl.h"
 #include "flrl_internal.hpp"
+#include "flrl_tuning.hpp"
 #include "flrl_outfile.hpp"
 
 namespace flrl {
@@ -726,26 +727,17 @@ std::vector<int> all_devices(int ndev)
 
 // Host-buffer FL (flrl_fl_compress / flrl_fl_decompress, flrl_fl.hip): the
 // same pipelines memory to memory on the current device, kHostWorkers wide.
-// Measured on 2 GiB u8 (scripts/bench_stream.py --mem-only --sweep, DESIGN.md
-// §4): the first touch of the freshly malloc'd output pages bounds the call
+// Measured on 2 GiB u8 (scripts/bench_stream.py --mem-only over variant
+// builds of the FLRL_HOST_* knobs, flrl_tuning.hpp): the first touch of the freshly malloc'd output pages bounds the call
 // (~10 GB/s single-threaded), not PCIe (57 GB/s each way); huge pages for the
 // outputs roughly double the rate; 8 pipelines x 16 MiB chunks through pinned
 // staging beat direct hipMemcpyAsync from/to the pageable buffers.
-constexpr int kHostWorkers = 8;
-constexpr size_t kHostChunk = 16ull << 20;
+constexpr int kHostWorkers = FLRL_HOST_WORKERS;
+constexpr size_t kHostChunk = FLRL_HOST_CHUNK;
 struct HostCfg {
     int workers = kHostWorkers;
-    size_t chunk = kHostChunk;
-    bool direct = false;
-    HostCfg()
-    {  // A/B overrides (scripts/bench_stream.py)
-        if (const char *v = getenv("FLRL_HOST_WORKERS"))
-            workers = atoi(v) > 0 ? atoi(v) : workers;
-        if (const char *v = getenv("FLRL_HOST_CHUNK"))
-            chunk = strtoull(v, nullptr, 0) >= kFrame ? chunk_size(strtoull(v, nullptr, 0)) : chunk;
-        if (const char *v = getenv("FLRL_HOST_DIRECT"))
-            direct = atoi(v) != 0;
-    }
+    size_t chunk = chunk_size(kHostChunk);
+    bool direct = FLRL_HOST_DIRECT != 0;
 };
 
 // malloc for a large host output, backed by transparent huge pages where the
@@ -754,8 +746,7 @@ struct HostCfg {
 uint8_t *host_alloc(size_t bytes)
 {
     uint8_t *p = static_cast<uint8_t *>(malloc(bytes ? bytes : 1));
-    const char *thp = getenv("FLRL_HOST_THP");  // "0": plain pages (A/B)
-    if (p && bytes >= (8u << 20) && !(thp && atoi(thp) == 0)) {
+    if (p && bytes >= (8u << 20) && FLRL_HOST_THP) {
         const uintptr_t a = ((uintptr_t)p + (2u << 20) - 1) & ~(uintptr_t)((2u << 20) - 1);
         const uintptr_t e = ((uintptr_t)p + bytes) & ~(uintptr_t)((2u << 20) - 1);
         if (e > a)

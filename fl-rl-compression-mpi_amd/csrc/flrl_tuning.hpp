@@ -13,7 +13,8 @@
     (defined(FLRL_RL_TRACE) || defined(FLRL_RL_LB_STAT) || defined(FLRL_FL_TRACE) ||                \
      defined(FLRL_RL_LB) || defined(FLRL_RL_THREADS) || defined(FLRL_RL_LOOKG) ||                   \
      defined(FLRL_RL_STAGE) || defined(FLRL_RD_NARROW_MEAN) || defined(FLRL_RL_RO_MAXB) ||          \
-     defined(FLRL_RD_UNROLL) || defined(FLRL_RL_WD64_MEAN) || defined(FLRL_RL_DENSE_MEAN))
+     defined(FLRL_RD_UNROLL) || defined(FLRL_HOST_WORKERS) || defined(FLRL_HOST_CHUNK) ||                \
+     defined(FLRL_HOST_DIRECT) || defined(FLRL_HOST_THP) || defined(FLRL_RL_WD64_MEAN) || defined(FLRL_RL_DENSE_MEAN))
 #error "FLRL_* kernel overrides are for timing harnesses only (define FLRL_TUNING_BUILD)"
 #endif
 
@@ -71,4 +72,21 @@
 #endif
 #ifndef FLRL_RL_DENSE_MEAN
 #define FLRL_RL_DENSE_MEAN 12
+#endif
+
+// ---- host-buffer API pipelines (flrl_fl_compress / flrl_fl_decompress) ------
+// 8 pipelines x 16 MiB chunks through pinned staging, outputs on transparent
+// huge pages (2 GiB u8: the first touch of fresh output pages bounds the call,
+// not PCIe); DIRECT 1 copies from/to the caller's pageable buffers instead.
+#ifndef FLRL_HOST_WORKERS
+#define FLRL_HOST_WORKERS 8
+#endif
+#ifndef FLRL_HOST_CHUNK
+#define FLRL_HOST_CHUNK (16ull << 20)
+#endif
+#ifndef FLRL_HOST_DIRECT
+#define FLRL_HOST_DIRECT 0
+#endif
+#ifndef FLRL_HOST_THP
+#define FLRL_HOST_THP 1
 #endif

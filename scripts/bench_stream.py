@@ -11,6 +11,8 @@ timed around the raw C calls) next to the PCIe copy ceiling (torch copies of
 the same bytes between pinned host memory and HBM). Prints one JSON line. Not
 part of bench.py's metric (that one is device-resident).
 Usage: bench_stream.py [--bytes N] [--kind u8] [--dir DIR] [--reps R] [--mem-only]
+(the host pipelines' shape is compile-time: FLRL_HOST_* in csrc/flrl_tuning.hpp,
+A/B by variant builds, scripts/build_variant.sh)
 """
 import argparse
 import json
@@ -110,18 +112,7 @@ def main():
     ap.add_argument("--dir", default=None)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--mem-only", action="store_true")
-    ap.add_argument("--sweep", action="store_true",
-                    help="with --mem-only: host API rates over FLRL_HOST_{DIRECT,WORKERS,CHUNK}")
     a = ap.parse_args()
-    if a.mem_only and a.sweep:
-        for thp in ("0", "1"):
-            for direct in ("0", "1"):
-                for w, ch in (("4", str(16 << 20)), ("8", str(16 << 20)), ("8", str(32 << 20))):
-                    os.environ.update(FLRL_HOST_DIRECT=direct, FLRL_HOST_WORKERS=w, FLRL_HOST_CHUNK=ch,
-                                      FLRL_HOST_THP=thp)
-                    r = mem_rates(a.bytes, a.kind, a.reps, ceiling=False)
-                    print(json.dumps({"thp": thp, "direct": direct, "workers": w, "chunk": ch, **r}), flush=True)
-        return
     if a.mem_only:
         print(json.dumps(mem_rates(a.bytes, a.kind, a.reps)))
         return
