@@ -48,11 +48,14 @@
 namespace flrl {
 
 constexpr int kRlThreads = FLRL_RL_THREADS;         // encode workgroup: 4 waves (LB 64: 94 VGPRs, < 32 KiB LDS, 5 per CU)
-constexpr int kRlLaneBytes = FLRL_RL_LB;            // contiguous bytes per lane (64 or 128)
+constexpr int kRlLaneBytes = 64;                    // contiguous bytes per lane (a u64 head mask)
 constexpr int kRlSub = 32768 / (64 * kRlLaneBytes); // sub-chunks per wave chunk (one look-back per tile)
 constexpr int kRlTileBytes = kRlLaneBytes * kRlThreads * kRlSub;  // 128 KiB: 4 waves x 32 KiB
 constexpr int kRlLookG = FLRL_RL_LOOKG;  // look-back granules per lane (window 64 G tiles)
 constexpr int kRlStageBytes = FLRL_RL_STAGE;  // LDS run staging per workgroup
+// 5 workgroups of 4 waves per CU (LDS-bound: < 32 KiB each): 5 waves per SIMD,
+// so at most 96 VGPRs
+constexpr int kRlWavesPerSimd = FLRL_RL_WPS;
 
 // Block decode workgroups: 512 threads over 8192-run tiles, 2 per CU, unless the
 // mean run is at least kRdNarrowMean bytes (runs near the 255 maximum: little
@@ -291,6 +294,65 @@ __device__ __forceinline__ uint64_t lookback_seg(uint64_t *status, uint32_t tile
     }
 }
 
+// Bytes [lo, hi) of the 16-byte chunk v (0 <= lo < hi <= 16) stored at dst (16-byte
+// aligned) as naturally aligned pieces: 1, 2, 4, 8 bytes up to a 16-byte
+// boundary, then 8, 4, 2, 1 while they fit.
+__device__ __forceinline__ void store_chunk_part(uint8_t *dst, u32x4 v, uint32_t lo, uint32_t hi)
+{
+    auto dw = [&](uint32_t a) { return a < 8 ? (a < 4 ? v[0] : v[1]) : (a < 12 ? v[2] : v[3]); };
+    auto qw = [&](uint32_t a) {
+        return a < 8 ? ((uint64_t)v[1] << 32) | v[0] : ((uint64_t)v[3] << 32) | v[2];
+    };
+    uint32_t a = lo;
+    if ((a & 1u) && a + 1 <= hi) {
+        dst[a] = (uint8_t)(dw(a) >> (8 * (a & 3)));
+        a += 1;
+    }
+    if ((a & 2u) && a + 2 <= hi) {
+        *reinterpret_cast<uint16_t *>(dst + a) = (uint16_t)(dw(a) >> (8 * (a & 3)));
+        a += 2;
+    }
+    if ((a & 4u) && a + 4 <= hi) {
+        *reinterpret_cast<uint32_t *>(dst + a) = dw(a);
+        a += 4;
+    }
+    if ((a & 8u) && a + 8 <= hi) {
+        *reinterpret_cast<uint64_t *>(dst + a) = qw(a);
+        a += 8;
+    }
+    if (a + 8 <= hi) {
+        *reinterpret_cast<uint64_t *>(dst + a) = qw(a);
+        a += 8;
+    }
+    if (a + 4 <= hi) {
+        *reinterpret_cast<uint32_t *>(dst + a) = dw(a);
+        a += 4;
+    }
+    if (a + 2 <= hi) {
+        *reinterpret_cast<uint16_t *>(dst + a) = (uint16_t)(dw(a) >> (8 * (a & 3)));
+        a += 2;
+    }
+    if (a + 1 <= hi)
+        dst[a] = (uint8_t)(dw(a) >> (8 * (a & 3)));
+}
+
+// Wave-uniform values held in scalar registers (the compiler cannot prove
+// that values read from LDS or derived from the wave index are uniform).
+__device__ __forceinline__ uint32_t uniform32(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
+__device__ __forceinline__ uint64_t uniform64(uint64_t v)
+{
+    return ((uint64_t)uniform32((uint32_t)(v >> 32)) << 32) | uniform32((uint32_t)v);
+}
+
+// LDS operations of one wave complete in order; the fences keep the compiler
+// from moving this wave's LDS accesses across this point.
+__device__ __forceinline__ void wave_lds_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // RL encode, per wave. A tile is 128 KiB; wave w of its workgroup owns the w-th
 // contiguous 32 KiB chunk and streams it as SUB sub-chunks of 64*LB bytes
 // through its OWN slice of LDS (registers -> ds_write -> each lane reads its LB
@@ -316,7 +378,9 @@ struct RlWave {
     static constexpr int NJ = WB / 1024;    // 1 KiB wave-loads per sub-chunk
     static constexpr int RPL = 1024 / LB;   // image rows per wave-load
     static constexpr uint32_t kNone = 0xFFFFFFFFu;
-    static_assert(LB == 128 || LB == 64, "one or two u64 head masks per lane");
+    // LDS per workgroup: W images and the run staging
+    static constexpr int kLdsBytes = W * WB + kRlStageBytes;
+    static_assert(LB == 64, "one u64 head mask per lane (piece emission: 4 x 16 positions)");
     static_assert(TBT == kRlTileBytes, "tile geometry shared with the layout");
 
     struct Sub {
@@ -353,8 +417,9 @@ struct RlWave {
     // ds_read_b128 (rows r..r+15, one chunk each) then cover all 64 banks
     __device__ static uint32_t swz(uint32_t r) { return LB == 128 ? (r & 7u) : ((r >> 2) & 3u); }
 
-    __device__ RlWave(const uint8_t *in_, uint64_t n_, uint8_t *lds, int w) : in(in_), n(n_)
+    __device__ RlWave(const uint8_t *in_, uint64_t n_, uint8_t *lds, int w_) : in(in_), n(n_)
     {
+        const int w = (int)uniform32((uint32_t)w_);
         lane = threadIdx.x & (kWave - 1);
         img = lds + w * WB;
         stc = lds + W * WB + w * 2 * SW;
@@ -490,6 +555,102 @@ struct RlWave {
         }
     }
 
+    // Dense emission (a sub-chunk with more records than the staging holds),
+    // part p: rows 16p .. 16p+15 of the image (row r = lane r's 64 bytes, head
+    // mask hm, state c_lane before it, first record at `slot`, byte before it
+    // p0 -- all held by lane r). Lane t takes piece k = t mod 4 (positions 16k
+    // .. 16k+15) of row 16p + t / 4, so every lane is busy whatever the density,
+    // and walks its 16 positions unrolled: values from the piece's bytes in
+    // registers, counts from the previous head's position (or the row's state
+    // before its first head). (Branch-free stores through a sink address for
+    // non-heads: runs32 +3 %, random bytes +12 %.) Record j of the part (j = record - base < 1024) goes to
+    // stc/stv[pswz(j)]: the swizzle spreads the 64 lanes' stores, 16 rows x 4
+    // pieces about 64 records apart, over all 64 banks. (Replaced one-row-at-
+    // a-time emission, whose readlane/rank work per row made dense inputs 3.7x
+    // slower than without it.)
+    __device__ static uint32_t pswz(uint32_t j) { return j ^ (((j >> 8) & 3u) << 2); }
+    __device__ void piece_part(int p, uint64_t hm, uint32_t c_lane, uint32_t slot, uint32_t p0, uint32_t base) const
+    {
+        const int k = lane & 3;
+        const int r = 16 * p + (lane >> 2);
+        const int src = r * 4;  // ds_bpermute address of lane r
+        const uint32_t mlo = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)hm);
+        const uint32_t mhi = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)(hm >> 32));
+        const uint32_t sr = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)slot);
+        const uint32_t cr = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)c_lane);
+        const uint32_t pr = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)p0);
+        const uint64_t m = ((uint64_t)mhi << 32) | mlo;
+        const u32x4 x = *reinterpret_cast<const u32x4 *>(img + (uint32_t)r * LB + (((uint32_t)k ^ swz((uint32_t)r)) * 16));
+        const uint32_t up = wave_shr1(x.w >> 24);  // lane t-1 holds piece k-1 of the same row when k > 0
+        const uint32_t pb = k == 0 ? pr : up;      // the byte before the piece
+        const uint64_t below = k == 0 ? 0ull : m & ((1ull << (16 * k)) - 1);
+        uint32_t rank = sr + (uint32_t)__popcll(below) - base;
+        // count of a head at pos = pos - prev; before the row's first head prev
+        // is -c (the state before the row): c + pos <= 255 by the 255-split rule
+        int32_t prev = below ? 63 - __builtin_clzll(below) : -(int32_t)cr;
+        const uint32_t m16 = (uint32_t)(m >> (16 * k)) & 0xFFFFu;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const bool h = (m16 >> i) & 1u;
+            const int32_t pos = 16 * k + i;
+            const uint32_t cnt = (uint32_t)(pos - prev);
+            const uint32_t val = i == 0 ? pb : (x[(i - 1) >> 2] >> (8 * ((i - 1) & 3))) & 0xFFu;
+            const uint32_t at = pswz(rank);
+            if (h) {
+                stc[at] = (uint8_t)(cnt == 0 ? 255u : cnt);
+                stv[at] = (uint8_t)val;
+            }
+            rank += h ? 1u : 0u;
+            prev = h ? pos : prev;
+        }
+    }
+
+    // 16 bytes of records o .. o+15 of a piece-staged array (pswz layout; o may
+    // be negative: those bytes read as 0 and are never stored)
+    __device__ static u32x4 piece_gather(const uint8_t *st, int32_t o)
+    {
+        const int32_t d = o >> 2;  // arithmetic: floor
+        const uint32_t sh = (uint32_t)o & 3u;
+        uint32_t w[5];
+#pragma unroll
+        for (int i = 0; i < 5; ++i)
+            w[i] = d + i < 0 ? 0u : *reinterpret_cast<const uint32_t *>(st + pswz(4u * (uint32_t)(d + i)));
+        return u32x4{__builtin_amdgcn_alignbyte(w[1], w[0], sh), __builtin_amdgcn_alignbyte(w[2], w[1], sh),
+                     __builtin_amdgcn_alignbyte(w[3], w[2], sh), __builtin_amdgcn_alignbyte(w[4], w[3], sh)};
+    }
+
+    // Records [0, nrec) of a piece-staged part to counts/values at global record
+    // index g0 + j, i.e. byte g0 + j - 1 (the input's first head, g0 + j == 0,
+    // ends no run): one 16-byte store per lane and array for every aligned
+    // chunk inside the range, 1/2/4/8-byte pieces for the two it shares.
+    __device__ void piece_flush(uint32_t nrec, uint64_t g0, uint8_t *__restrict__ counts,
+                                uint8_t *__restrict__ values) const
+    {
+        const uint32_t j0 = g0 == 0 ? 1u : 0u;
+        if (nrec <= j0)
+            return;
+        // destination bytes [A, E) = [g0 + j0 - 1, g0 + nrec - 1), in 16-byte
+        // chunks from the one holding A; chunk q starts at record (q - h) * 16 - a
+        const uint64_t A = g0 + j0 - 1;
+        const uint32_t a = (uint32_t)(A & 15u);  // A's offset in its chunk
+        const uint32_t span = a + (nrec - j0);   // bytes from the chunk start to E
+        uint8_t *const pc = counts + (A - a), *const pv = values + (A - a);
+        for (uint32_t q = (uint32_t)lane; 16 * q < span; q += kWave) {
+            const int32_t o = (int32_t)(16 * q) - (int32_t)a + (int32_t)j0;  // record of the chunk's first byte
+            const uint32_t lo = q == 0 ? a : 0u;
+            const uint32_t hi = span - 16 * q < 16 ? span - 16 * q : 16u;
+#pragma unroll
+            for (int arr = 0; arr < 2; ++arr) {
+                const u32x4 v = piece_gather(arr ? stv : stc, o);
+                uint8_t *const d = (arr ? pv : pc) + 16 * q;
+                if (lo == 0 && hi == 16)
+                    *reinterpret_cast<u32x4 *>(d) = v;
+                else
+                    store_chunk_part(d, v, lo, hi);
+            }
+        }
+    }
+
     // The staging pass over the chunk at `off` (`len` bytes): every sub-chunk's
     // PhaseMap and natural heads; the runs of the state-independent heads are
     // staged in LDS (stc/stv) at their chunk-local index until the staging area
@@ -593,6 +754,70 @@ struct RlWave {
         }
     }
 
+    // Sub-chunks [s0, ns) of the chunk at `off`, re-read and emitted with the
+    // true states: hb = the global index of sub-chunk s0's first record, rel =
+    // the PhaseMap from the chunk start to s0, c_in = the chunk's incoming state.
+    __device__ void reread(uint64_t off, int s0, int ns, uint64_t hb, uint32_t rel, uint32_t c_in,
+                           uint8_t *__restrict__ counts, uint8_t *__restrict__ values) const
+    {
+        off = uniform64(off);
+        hb = uniform64(hb);
+        rel = uniform32(rel);
+        c_in = uniform32(c_in);
+        const uint64_t re_off = off + (uint64_t)s0 * WB;
+        uint32_t pb = uniform32(re_off > 0 ? (uint32_t)in[re_off - 1] : 0u);
+        u32x4 pf[NJ];
+        load_sub(off, s0, pf);
+        for (int s = s0; s < ns; ++s) {
+            // the previous sub-chunk's reads of the staging and the image are
+            // this wave's own LDS ops: in order
+            Sub L;
+            pb = scan_sub(off, s, L, pf, pb, false);
+#pragma unroll
+            for (int j = 0; j < NJ; ++j)
+                pf[j] = u32x4{0u, 0u, 0u, 0u};  // consumed: not live until the next load
+            const uint32_t c_lane = pm_apply(pm_compose(rel, L.lrel), c_in);
+            uint64_t hm0, hm1;
+            head_masks(L, c_lane, true, hm0, hm1);
+            const uint32_t hl = (uint32_t)(__popcll(hm0) + __popcll(hm1));
+            const uint32_t hincl = wave_incl_scan_u32(hl);
+            const uint32_t hs = (uint32_t)__builtin_amdgcn_readlane((int)hincl, kWave - 1);
+            const uint64_t g = hb + (hincl - hl);
+            if (hs <= (uint32_t)SW) {
+                // stage at (g - hb), store contiguously
+                if (s + 1 < ns)
+                    load_sub(off, s + 1, pf);
+                lane_runs(L, hm0, hm1, c_lane, (uint32_t)(g - hb));
+                wave_lds_sync();
+                for (uint32_t j = lane; j < hs; j += kWave) {
+                    const uint64_t gi = hb + j;
+                    if (gi > 0) {
+                        counts[gi - 1] = stc[j];
+                        values[gi - 1] = stv[j];
+                    }
+                }
+                wave_lds_sync();
+            } else {
+                // four parts of 16 rows (<= 1024 records each, within the staging),
+                // each staged by piece_part and stored with 16-byte stores
+                const uint32_t sl = (uint32_t)(g - hb);
+#pragma unroll 1
+                for (int p = 0; p < kWave / 16; ++p) {
+                    const uint32_t b0 = (uint32_t)__builtin_amdgcn_readlane((int)sl, 16 * p);
+                    const uint32_t b1 = p + 1 < kWave / 16 ? (uint32_t)__builtin_amdgcn_readlane((int)sl, 16 * (p + 1)) : hs;
+                    piece_part(p, hm0, c_lane, sl, L.p0, b0);
+                    wave_lds_sync();
+                    piece_flush(b1 - b0, hb + b0, counts, values);
+                    wave_lds_sync();
+                }
+            }
+            if (hs > (uint32_t)SW && s + 1 < ns)
+                load_sub(off, s + 1, pf);  // after the pieces: see above
+            hb += hs;
+            rel = pm_compose(rel, L.smap);
+        }
+    }
+
     // Emission of chunk C with the state (heads before it, chunk state) at its
     // start; its staged records are in stc/stv. The wave whose chunk ends the
     // input also writes the final run and R.
@@ -601,6 +826,8 @@ struct RlWave {
     {
         if (C.ns == 0)
             return;
+        h_in = uniform64(h_in);
+        c_in = uniform32(c_in);
         const uint32_t pre = C.pre();
         {
             // staged sub-chunks [0, nst): split heads h_in + j end full 255-byte
@@ -628,85 +855,12 @@ struct RlWave {
             }
         }
         if (C.nst < C.ns) {
-            // sub-chunks [nst, ns): re-read and emit with the true states
-            uint32_t rel = C.rel_st;
-            uint64_t hb = h_in + splits(c_in, pre < (uint32_t)C.nst * WB ? pre : (uint32_t)C.nst * WB) + C.Kst;
-            const uint64_t re_off = C.off + (uint64_t)C.nst * WB;
-            uint32_t pb = re_off > 0 ? (uint32_t)in[re_off - 1] : 0u;
-            u32x4 pf[NJ];
-            load_sub(C.off, C.nst, pf);
-            for (int s = C.nst; s < C.ns; ++s) {
-                // the staged copy-out above and the previous sub-chunk's reads of the
-                // staging and the image are this wave's own LDS ops: in order
-                Sub L;
-                pb = scan_sub(C.off, s, L, pf, pb, s + 1 < C.ns);
-                const uint32_t c_lane = pm_apply(pm_compose(rel, L.lrel), c_in);
-                uint64_t hm0, hm1;
-                head_masks(L, c_lane, true, hm0, hm1);
-                const uint32_t hl = (uint32_t)(__popcll(hm0) + __popcll(hm1));
-                const uint32_t hincl = wave_incl_scan_u32(hl);
-                const uint32_t hs = (uint32_t)__builtin_amdgcn_readlane((int)hincl, kWave - 1);
-                const uint64_t g = hb + (hincl - hl);
-                if (hs <= (uint32_t)SW) {
-                    // sparse: stage at (g - hb), store contiguously
-                    lane_runs(L, hm0, hm1, c_lane, (uint32_t)(g - hb));
-                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                    __builtin_amdgcn_wave_barrier();
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                    for (uint32_t j = lane; j < hs; j += kWave) {
-                        const uint64_t gi = hb + j;
-                        if (gi > 0) {
-                            counts[gi - 1] = stc[j];
-                            values[gi - 1] = stv[j];
-                        }
-                    }
-                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                    __builtin_amdgcn_wave_barrier();
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                } else {
-                    // dense: ONE lane row at a time, lane t taking byte positions t
-                    // and 64 + t of the row (ranks by popcount): contiguous stores
-                    const uint64_t below = ((uint64_t)1 << lane) - 1;
-#pragma unroll 1
-                    for (int r = 0; r < kWave; ++r) {
-                        const uint64_t h0 = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(hm0 >> 32), r) << 32) |
-                                            (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)hm0, r);
-                        const uint64_t h1 = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(hm1 >> 32), r) << 32) |
-                                            (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)hm1, r);
-                        const uint64_t g_row = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(g >> 32), r) << 32) |
-                                               (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)g, r);
-                        const uint32_t c_row = (uint32_t)__builtin_amdgcn_readlane((int)c_lane, r);
-                        const uint32_t p_row = (uint32_t)__builtin_amdgcn_readlane((int)L.p0, r);
-                        const uint32_t rr = (uint32_t)r;
-                        const uint8_t *rowp = img + rr * LB;
-#pragma unroll
-                        for (int half = 0; half < CH / 4; ++half) {
-                            const uint64_t hm = half ? h1 : h0;
-                            if ((hm >> lane) & 1u) {
-                                const uint64_t bl = hm & below;
-                                const uint32_t pos = (uint32_t)(half * 64 + lane);
-                                const uint32_t rank = (half ? (uint32_t)__popcll(h0) : 0u) + (uint32_t)__popcll(bl);
-                                int prev;
-                                if (bl)
-                                    prev = half * 64 + 63 - __builtin_clzll(bl);
-                                else
-                                    prev = (half && h0) ? 63 - __builtin_clzll(h0) : -1;
-                                uint32_t cnt = prev < 0 ? add_c(c_row, pos) : pos - (uint32_t)prev;
-                                cnt = cnt == 0 ? 255u : cnt;
-                                const uint32_t q = pos - 1;
-                                const uint32_t val = pos == 0 ? p_row : rowp[(((q >> 4) ^ swz(rr)) * 16) + (q & 15u)];
-                                const uint64_t gi = g_row + rank;
-                                if (gi > 0) {
-                                    counts[gi - 1] = (uint8_t)cnt;
-                                    values[gi - 1] = (uint8_t)val;
-                                }
-                            }
-                        }
-                    }
-                }
-                hb += hs;
-                rel = pm_compose(rel, L.smap);
-            }
+            // sub-chunks [nst, ns) overflowed the staging: re-read and emitted
+            // with the true states (the tile was read a few microseconds ago:
+            // the re-read mostly hits the caches; deferring it to a second
+            // kernel, which re-reads from HBM, was 1.4-1.9x slower on dense inputs)
+            const uint64_t hb = h_in + splits(c_in, pre < (uint32_t)C.nst * WB ? pre : (uint32_t)C.nst * WB) + C.Kst;
+            reread(C.off, C.nst, C.ns, hb, C.rel_st, c_in, counts, values);
         }
         // the final run (ends at byte n-1): the wave whose chunk holds it
         if (C.off + C.len == n && lane == 0) {
@@ -723,13 +877,13 @@ struct RlWave {
 // tile map, ONE look-back by wave 0 while waves 1-3 wait, emit. Three block
 // barriers per tile (ticket, wave maps, state).
 template <int T, int LB, int SUB>
-__global__ __launch_bounds__(T) void rl_encode_wave_kernel(
+__global__ __launch_bounds__(T, kRlWavesPerSimd) void rl_encode_wave_kernel(  // (2nd: waves per SIMD)
     const uint8_t *__restrict__ in, uint64_t n, uint32_t ntiles, uint8_t *__restrict__ counts,
     uint8_t *__restrict__ values, uint64_t *__restrict__ runs_out, Ctrl *ctrl, uint64_t *status)
 {
     constexpr int W = T / kWave;
     using Wv = RlWave<LB, SUB, W>;
-    __shared__ __attribute__((aligned(16))) uint8_t s_lds[W * Wv::WB + kRlStageBytes];
+    __shared__ __attribute__((aligned(16))) uint8_t s_lds[Wv::kLdsBytes];
     __shared__ uint64_t s_map[W];
     __shared__ uint64_t s_st[W];
     __shared__ uint32_t s_ticket;
@@ -818,13 +972,13 @@ struct RlChunkSum {  // a wave's Chunk in 48 bytes
 };
 
 template <int T, int LB, int SUB>
-__global__ __launch_bounds__(T) void rl_encode_scan_kernel(const uint8_t *__restrict__ in, uint64_t n,
+__global__ __launch_bounds__(T, kRlWavesPerSimd) void rl_encode_scan_kernel(const uint8_t *__restrict__ in, uint64_t n,
                                                            uint64_t *__restrict__ tmap, u32x4 *__restrict__ sums,
                                                            uint8_t *__restrict__ gstage)
 {
     constexpr int W = T / kWave;
     using Wv = RlWave<LB, SUB, W>;
-    __shared__ __attribute__((aligned(16))) uint8_t s_lds[W * Wv::WB + kRlStageBytes];
+    __shared__ __attribute__((aligned(16))) uint8_t s_lds[Wv::kLdsBytes];
     __shared__ uint64_t s_map[W];
     const int w = threadIdx.x / kWave;
     const Wv V(in, n, s_lds, w);
@@ -834,9 +988,7 @@ __global__ __launch_bounds__(T) void rl_encode_scan_kernel(const uint8_t *__rest
     const uint32_t len = off >= n ? 0u : (n - off < (uint64_t)Wv::CB ? (uint32_t)(n - off) : (uint32_t)Wv::CB);
     V.scan_chunk(off, len, C, [](int) {});
     uint8_t *gs = gstage + (uint64_t)tile * kRlStageBytes + (uint64_t)w * 2 * Wv::SW;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the staging writes of all lanes first
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    wave_lds_sync();  // the staging writes of all lanes first
     V.staging_to(gs, gs + Wv::SW, C.Kst);
     if (V.lane == 0) {
         RlChunkSum<LB, SUB, W>::put(sums + ((uint64_t)tile * W + w) * 3, C);
@@ -960,7 +1112,7 @@ __global__ __launch_bounds__(kRsThreads) void rl_encode_state_kernel(const uint6
 }
 
 template <int T, int LB, int SUB>
-__global__ __launch_bounds__(T) void rl_encode_emit_kernel(const uint8_t *__restrict__ in, uint64_t n,
+__global__ __launch_bounds__(T, kRlWavesPerSimd) void rl_encode_emit_kernel(const uint8_t *__restrict__ in, uint64_t n,
                                                            const u32x4 *__restrict__ sums,
                                                            const uint64_t *__restrict__ tlocal,
                                                            const uint64_t *__restrict__ bpre,
@@ -971,7 +1123,7 @@ __global__ __launch_bounds__(T) void rl_encode_emit_kernel(const uint8_t *__rest
     constexpr int W = T / kWave;
     using Wv = RlWave<LB, SUB, W>;
     using Sum = RlChunkSum<LB, SUB, W>;
-    __shared__ __attribute__((aligned(16))) uint8_t s_lds[W * Wv::WB + kRlStageBytes];
+    __shared__ __attribute__((aligned(16))) uint8_t s_lds[Wv::kLdsBytes];
     const int w = threadIdx.x / kWave;
     const Wv V(in, n, s_lds, w);
     const uint32_t tile = blockIdx.x;
@@ -983,9 +1135,7 @@ __global__ __launch_bounds__(T) void rl_encode_emit_kernel(const uint8_t *__rest
     const typename Wv::Chunk C = Sum::get(ts + 3 * w);
     const uint8_t *gs = gstage + (uint64_t)tile * kRlStageBytes + (uint64_t)w * 2 * Wv::SW;
     V.staging_from(gs, gs + Wv::SW, C.Kst);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    wave_lds_sync();
     V.emit(C, sm_h(st), sm_c(st), counts, values, runs_out);
 }
 
@@ -1129,48 +1279,6 @@ __global__ __launch_bounds__(kRoThreads, 4) void rl_offsets_kernel(  // 4 workgr
         if (base - wbase + local != n)
             raise_error(ctrl, FLRL_E_FORMAT);
     }
-}
-
-// Bytes [lo, hi) of the 16-byte chunk v (0 <= lo < hi <= 16) stored at dst (16-byte
-// aligned) as naturally aligned pieces: 1, 2, 4, 8 bytes up to a 16-byte
-// boundary, then 8, 4, 2, 1 while they fit.
-__device__ __forceinline__ void store_chunk_part(uint8_t *dst, u32x4 v, uint32_t lo, uint32_t hi)
-{
-    auto dw = [&](uint32_t a) { return a < 8 ? (a < 4 ? v[0] : v[1]) : (a < 12 ? v[2] : v[3]); };
-    auto qw = [&](uint32_t a) {
-        return a < 8 ? ((uint64_t)v[1] << 32) | v[0] : ((uint64_t)v[3] << 32) | v[2];
-    };
-    uint32_t a = lo;
-    if ((a & 1u) && a + 1 <= hi) {
-        dst[a] = (uint8_t)(dw(a) >> (8 * (a & 3)));
-        a += 1;
-    }
-    if ((a & 2u) && a + 2 <= hi) {
-        *reinterpret_cast<uint16_t *>(dst + a) = (uint16_t)(dw(a) >> (8 * (a & 3)));
-        a += 2;
-    }
-    if ((a & 4u) && a + 4 <= hi) {
-        *reinterpret_cast<uint32_t *>(dst + a) = dw(a);
-        a += 4;
-    }
-    if ((a & 8u) && a + 8 <= hi) {
-        *reinterpret_cast<uint64_t *>(dst + a) = qw(a);
-        a += 8;
-    }
-    if (a + 8 <= hi) {
-        *reinterpret_cast<uint64_t *>(dst + a) = qw(a);
-        a += 8;
-    }
-    if (a + 4 <= hi) {
-        *reinterpret_cast<uint32_t *>(dst + a) = dw(a);
-        a += 4;
-    }
-    if (a + 2 <= hi) {
-        *reinterpret_cast<uint16_t *>(dst + a) = (uint16_t)(dw(a) >> (8 * (a & 3)));
-        a += 2;
-    }
-    if (a + 1 <= hi)
-        dst[a] = (uint8_t)(dw(a) >> (8 * (a & 3)));
 }
 
 // One 16-byte output chunk of a rank-decode window (block and wave decode):
@@ -1493,14 +1601,6 @@ constexpr uint64_t kWdDenseMean = FLRL_RL_DENSE_MEAN;
 static_assert(kWdWords == 4 * kWave, "one bitmap vector per lane");
 
 
-__device__ __forceinline__ void wave_lds_sync()
-{
-    // LDS operations of one wave complete in order; the fences keep the
-    // compiler from moving LDS accesses across this point
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
 
 template <int RPL>
 __global__ __launch_bounds__(kWdThreads) void rl_decode_wave_kernel(
@@ -1653,18 +1753,20 @@ __global__ __launch_bounds__(kWdThreads) void rl_decode_wave_kernel(
 // [tmap: tiles][tlocal: tiles][bagg: blocks x 32 B][bpre: blocks x 16 B]
 // [sums: tiles x 4 x 48 B][staged runs: tiles x kRlStageBytes]
 struct RlEncLayout {
-    size_t tiles, sblocks, zero, o_tmap, o_tstate, o_bagg, o_bpre, o_sums, o_stage, bytes;
+    size_t tiles, sblocks, zero, o_status, o_tmap, o_tstate, o_bagg, o_bpre, o_sums, o_stage, bytes;
     explicit RlEncLayout(size_t n, bool three)
     {
         tiles = div_up(n, (size_t)kRlTileBytes);
         if (!three) {
             sblocks = 0;
+            o_status = sizeof(Ctrl);
             zero = sizeof(Ctrl) + round_up(tiles * 8, 16);  // ticket, error, status granules
             o_tmap = o_tstate = o_bagg = o_bpre = o_sums = o_stage = bytes = zero;
             return;
         }
         sblocks = div_up(tiles, (size_t)kRsThreads);
         zero = sizeof(Ctrl);  // the state kernel's block counter
+        o_status = zero;
         o_tmap = zero;
         o_tstate = o_tmap + round_up(tiles * 8, 16);   // tlocal
         o_bagg = o_tstate + round_up(tiles * 8, 16);
@@ -1745,16 +1847,15 @@ extern "C" int flrl_rl_encode_device_form(const uint8_t *d_in, size_t n, uint8_t
     if (L.tiles > 0xFFFFFFFFull)
         return set_error(FLRL_E_ARG, "flrl_rl_encode_device: input too large");
     Ctrl *ctrl = static_cast<Ctrl *>(d_scratch);
-    uint64_t *status = reinterpret_cast<uint64_t *>(ctrl + 1);
+    uint8_t *base = static_cast<uint8_t *>(d_scratch);
+    kernel_timing_begin(s);  // the hook brackets every pass of the encode
     if (three) {
-        uint8_t *base = static_cast<uint8_t *>(d_scratch);
         uint64_t *tmap = reinterpret_cast<uint64_t *>(base + L.o_tmap);
         uint64_t *tlocal = reinterpret_cast<uint64_t *>(base + L.o_tstate);
         uint64_t *bagg = reinterpret_cast<uint64_t *>(base + L.o_bagg);
         uint64_t *bpre = reinterpret_cast<uint64_t *>(base + L.o_bpre);
         u32x4 *sums = reinterpret_cast<u32x4 *>(base + L.o_sums);
         uint8_t *stage = base + L.o_stage;
-        kernel_timing_begin(s);  // the hook brackets all three passes
         hipLaunchKernelGGL((rl_encode_scan_kernel<kRlThreads, kRlLaneBytes, kRlSub>), dim3((uint32_t)L.tiles),
                            dim3(kRlThreads), 0, s, d_in, (uint64_t)n, tmap, sums, stage);
         hipLaunchKernelGGL(rl_encode_state_kernel, dim3((uint32_t)L.sblocks), dim3(kRsThreads), 0, s, tmap,
@@ -1762,14 +1863,12 @@ extern "C" int flrl_rl_encode_device_form(const uint8_t *d_in, size_t n, uint8_t
         hipLaunchKernelGGL((rl_encode_emit_kernel<kRlThreads, kRlLaneBytes, kRlSub>), dim3((uint32_t)L.tiles),
                            dim3(kRlThreads), 0, s, d_in, (uint64_t)n, sums, tlocal, bpre, stage, d_counts,
                            d_values, d_runs);
-        kernel_timing_end(s);
-        FLRL_HIP(hipGetLastError());
-        return FLRL_OK;
+    } else {
+        uint64_t *status = reinterpret_cast<uint64_t *>(base + L.o_status);
+        hipLaunchKernelGGL((rl_encode_wave_kernel<kRlThreads, kRlLaneBytes, kRlSub>), dim3((uint32_t)L.tiles),
+                           dim3(kRlThreads), 0, s, d_in, (uint64_t)n, (uint32_t)L.tiles, d_counts, d_values,
+                           d_runs, ctrl, status);
     }
-    kernel_timing_begin(s);
-    hipLaunchKernelGGL((rl_encode_wave_kernel<kRlThreads, kRlLaneBytes, kRlSub>), dim3((uint32_t)L.tiles),
-                       dim3(kRlThreads), 0, s, d_in, (uint64_t)n, (uint32_t)L.tiles, d_counts, d_values,
-                       d_runs, ctrl, status);
     kernel_timing_end(s);
     FLRL_HIP(hipGetLastError());
     return FLRL_OK;

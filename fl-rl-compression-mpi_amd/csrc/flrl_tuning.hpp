@@ -11,8 +11,8 @@
 
 #if !defined(FLRL_TUNING_BUILD) &&                                                                  \
     (defined(FLRL_RL_TRACE) || defined(FLRL_RL_LB_STAT) || defined(FLRL_FL_TRACE) ||                \
-     defined(FLRL_RL_LB) || defined(FLRL_RL_THREADS) || defined(FLRL_RL_LOOKG) ||                   \
-     defined(FLRL_RL_STAGE) || defined(FLRL_RD_NARROW_MEAN) || defined(FLRL_RL_RO_MAXB) ||          \
+     defined(FLRL_RL_THREADS) || defined(FLRL_RL_LOOKG) ||                   \
+     defined(FLRL_RL_STAGE) || defined(FLRL_RL_WPS) || defined(FLRL_RD_NARROW_MEAN) || defined(FLRL_RL_RO_MAXB) ||          \
      defined(FLRL_RD_UNROLL) || defined(FLRL_HOST_WORKERS) || defined(FLRL_HOST_CHUNK) ||                \
      defined(FLRL_HOST_DIRECT) || defined(FLRL_HOST_THP) || defined(FLRL_RL_WD64_MEAN) || defined(FLRL_RL_DENSE_MEAN))
 #error "FLRL_* kernel overrides are for timing harnesses only (define FLRL_TUNING_BUILD)"
@@ -36,9 +36,6 @@
 #endif
 
 // ---- RL encode shape ---------------------------------------------------------
-#ifndef FLRL_RL_LB
-#define FLRL_RL_LB 64  // contiguous bytes per lane (64 or 128)
-#endif
 #ifndef FLRL_RL_THREADS
 #define FLRL_RL_THREADS 256  // 4 waves (LB 64: 94 VGPRs, < 32 KiB LDS, 5 per CU)
 #endif
@@ -47,6 +44,12 @@
 #endif
 #ifndef FLRL_RL_STAGE
 #define FLRL_RL_STAGE 15360  // LDS run staging per workgroup (bytes)
+#endif
+
+// RL encode: minimum waves per SIMD the kernels are compiled for (5: five
+// 4-wave workgroups per CU, at most 96 VGPRs).
+#ifndef FLRL_RL_WPS
+#define FLRL_RL_WPS 5
 #endif
 
 // ---- RL decode shape ---------------------------------------------------------
