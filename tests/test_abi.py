@@ -130,3 +130,21 @@ def test_rl_encode_unknown_form():
     # rejected before any device work (no GPU needed)
     rc = flrl.lib_handle().flrl_rl_encode_device_form(None, 0, None, None, None, None, 0, None, 2)
     assert rc == flrl.E_ARG
+
+
+def test_tuning_overrides_need_the_tuning_build(tmp_path):
+    """A kernel-shape override (-DFLRL_RL_STAGE=..., any FLRL_* knob of
+    csrc/flrl_tuning.hpp) is a compile error unless FLRL_TUNING_BUILD is also
+    defined, so a stray -D cannot change the shipped library; the shipped
+    defaults compile clean."""
+    inc = os.path.join(os.path.dirname(flrl.LIB_PATH), "..", "csrc")
+    src = tmp_path / "t.cpp"
+    src.write_text('#include "flrl_tuning.hpp"\nint main() { return FLRL_RL_STAGE > 0 ? 0 : 1; }\n')
+
+    def cc(*defs):
+        return subprocess.run(["g++", "-fsyntax-only", "-I", inc, *defs, str(src)], capture_output=True, text=True)
+
+    assert cc().returncode == 0
+    bad = cc("-DFLRL_RL_STAGE=1024")
+    assert bad.returncode != 0 and "FLRL_TUNING_BUILD" in bad.stderr
+    assert cc("-DFLRL_RL_STAGE=1024", "-DFLRL_TUNING_BUILD").returncode == 0
