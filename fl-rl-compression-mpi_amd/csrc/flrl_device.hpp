@@ -179,36 +179,31 @@ __device__ __forceinline__ uint32_t block_excl_scan(const TIn *s_in, uint32_t *s
     return total;
 }
 
-// A look-back window (lane i holds the status of tile j-i) is usable once every
-// slot up to and including the nearest inclusive prefix (P) is published; slots
-// beyond that P are not needed, so a straggler further back never stalls us.
-__device__ __forceinline__ bool window_ready(uint64_t s)
-{
-    const unsigned long long xm = __ballot((s >> 62) == 0);
-    const unsigned long long pm = __ballot((s >> 62) == 2);
-    if (!pm)
-        return xm == 0;
-    const unsigned long long upto = pm & (~pm + 1);  // lowest P lane
-    return (xm & ((upto << 1) - 1)) == 0;
-}
-
 // Decoupled look-back for an additive u64 scan (payload < 2^62), split in two
 // so a caller can publish its aggregate early and resolve its prefix later.
 // publish_aggregate: ONE lane stores the tile's aggregate (tile 0 publishes its
 // inclusive prefix directly).
+template <int S = 1>
 __device__ __forceinline__ void publish_aggregate(uint64_t *status, uint32_t tile, uint64_t agg)
 {
-    granule_store(&status[tile], (tile == 0 ? kFlagP : kFlagA) | agg);
+    granule_store(&status[(size_t)tile * S], (tile == 0 ? kFlagP : kFlagA) | agg);
 }
 
 // lookback_resolve: called by ONE full wave after publish_aggregate. Sums
-// predecessors 64 at a time until it meets an inclusive prefix, publishes the
-// tile's inclusive prefix and returns the exclusive prefix (to every lane).
+// predecessors 64 G at a time (lane i holds tiles j-iG .. j-iG-G+1) until it
+// meets an inclusive prefix (P), publishes the tile's inclusive prefix and
+// returns the exclusive prefix (to every lane). A window is usable once every
+// slot up to and including the nearest P is published; slots beyond that P are
+// not needed, so a straggler further back never stalls us. A wider window (G >
+// 1) resolves the first round of a launch -- every tile's predecessors are
+// aggregates back to tile 0 -- in fewer round trips.
 // Must stay inlined: a call makes the callee open with s_waitcnt vmcnt(0),
 // which would drain the caller's in-flight prefetch loads before the look-back.
+template <int G, int L = kWave, int S = 1>
 __device__ __forceinline__ uint64_t lookback_resolve(uint64_t *status, uint32_t tile, uint64_t agg,
                                                   Ctrl *ctrl)
 {
+    static_assert(L >= 1 && L <= kWave && (G == 1 || L == kWave), "window of L lanes x G granules");
     const int lane = threadIdx.x & (kWave - 1);
     if (tile == 0)
         return 0;
@@ -216,11 +211,33 @@ __device__ __forceinline__ uint64_t lookback_resolve(uint64_t *status, uint32_t 
     int64_t j = (int64_t)tile - 1;
     uint32_t spins = 0;
     for (;;) {
-        const int64_t idx = j - lane;
-        uint64_t s;
+        const int64_t idx = j - (int64_t)lane * G;
+        uint64_t part;
+        bool has_p;
         for (;;) {
-            s = idx >= 0 ? granule_load(&status[idx]) : kFlagP;
-            if (window_ready(s))
+            uint64_t s[G];
+#pragma unroll
+            for (int k = 0; k < G; ++k)
+                s[k] = lane >= L     ? kFlagA
+                       : idx - k >= 0 ? granule_load(&status[(idx - k) * S])
+                                      : kFlagP;
+            // lane-local: sum from the lane's newest slot back to its nearest P
+            has_p = false;
+            bool ok = true;
+            part = 0;
+#pragma unroll
+            for (int k = 0; k < G; ++k) {
+                if (!has_p) {
+                    const uint32_t f = (uint32_t)(s[k] >> 62);
+                    ok = ok && f != 0;
+                    has_p = f == 2;
+                    part += s[k] & kPayload;
+                }
+            }
+            const unsigned long long pm = __ballot(has_p);
+            const unsigned long long bad = __ballot(!ok);
+            const unsigned long long upto = pm ? ((pm & (~pm + 1)) << 1) - 1 : ~0ull;
+            if ((bad & upto) == 0)
                 break;
             if (++spins > kSpinLimit) {
                 if (lane == 0)
@@ -229,64 +246,16 @@ __device__ __forceinline__ uint64_t lookback_resolve(uint64_t *status, uint32_t 
             }
             __builtin_amdgcn_s_sleep(1);
         }
-        const unsigned long long pm = __ballot((s >> 62) == 2);
+        const unsigned long long pm = __ballot(has_p);
         const int first_p = pm ? __ffsll(pm) - 1 : kWave;
-        excl += wave_sum_u64(lane <= first_p ? (s & kPayload) : 0ull);
+        excl += wave_sum_u64(lane <= first_p ? part : 0ull);
         if (pm)
             break;
-        j -= kWave;
+        j -= (int64_t)L * G;
     }
     if (lane == 0)
-        granule_store(&status[tile], kFlagP | (excl + agg));
+        granule_store(&status[(size_t)tile * S], kFlagP | (excl + agg));
     return excl;
-}
-
-// As lookback_resolve, but the first window (tiles tile-1-lane) was already
-// loaded by the caller into `probe` — issue that load early (before long
-// streams of other vector-memory ops) so its wait does not queue behind them.
-__device__ __forceinline__ uint64_t lookback_resolve_probed(uint64_t *status, uint32_t tile,
-                                                            uint64_t agg, Ctrl *ctrl,
-                                                            uint64_t probe)
-{
-    const int lane = threadIdx.x & (kWave - 1);
-    if (tile == 0)
-        return 0;
-    uint64_t excl = 0;
-    int64_t j = (int64_t)tile - 1;
-    uint32_t spins = 0;
-    uint64_t s = probe;
-    for (;;) {
-        const int64_t idx = j - lane;
-        while (!window_ready(s)) {
-            if (++spins > kSpinLimit) {
-                if (lane == 0)
-                    raise_error(ctrl, FLRL_E_TIMEOUT);
-                return excl;
-            }
-            __builtin_amdgcn_s_sleep(1);
-            s = idx >= 0 ? granule_load(&status[idx]) : kFlagP;
-        }
-        const unsigned long long pm = __ballot((s >> 62) == 2);
-        const int first_p = pm ? __ffsll(pm) - 1 : kWave;
-        excl += wave_sum_u64(lane <= first_p ? (s & kPayload) : 0ull);
-        if (pm)
-            break;
-        j -= kWave;
-        const int64_t nidx = j - lane;
-        s = nidx >= 0 ? granule_load(&status[nidx]) : kFlagP;
-    }
-    if (lane == 0)
-        granule_store(&status[tile], kFlagP | (excl + agg));
-    return excl;
-}
-
-// Both halves in one call (ONE full wave).
-__device__ __forceinline__ uint64_t lookback_sum(uint64_t *status, uint32_t tile, uint64_t agg,
-                                                 Ctrl *ctrl)
-{
-    if ((threadIdx.x & (kWave - 1)) == 0)
-        publish_aggregate(status, tile, agg);
-    return lookback_resolve(status, tile, agg, ctrl);
 }
 
 // Exclusive prefix of per-workgroup aggregates for the pre-pass scans: the

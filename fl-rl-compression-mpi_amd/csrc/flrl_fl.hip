@@ -248,9 +248,9 @@ __global__ __launch_bounds__(T + kWave, 1) void fl_encode_kernel(
             // it issues no bulk loads or stores, so its status loads never wait
             // behind them -- vmcnt is per wave and in order)
             if (tid == T)
-                publish_aggregate(status, tile, agg);
+                publish_aggregate<FLRL_FL_STATUS_STRIDE>(status, tile, agg);
             FLRL_FL_TRACE(tile, 1);
-            const uint64_t excl = lookback_resolve(status, tile, agg, ctrl);
+            const uint64_t excl = lookback_resolve<FLRL_FL_LOOKG, FLRL_FL_LOOKL, FLRL_FL_STATUS_STRIDE>(status, tile, agg, ctrl);
             if (tid == T)
                 s_base = excl;
             FLRL_FL_TRACE(tile, 2);
@@ -619,7 +619,7 @@ struct FlLayout {
         off_iters = div_up(div_up(frames, (size_t)kOffFrames), (size_t)kMaxPrefixBlocks);
         off_iters = off_iters ? off_iters : 1;
         off_blocks = div_up(frames, (size_t)kOffFrames * off_iters);
-        enc_zero = sizeof(Ctrl) + round_up(enc_tiles * 8, 16);
+        enc_zero = FLRL_FL_STATUS_OFF + round_up(enc_tiles * 8 * FLRL_FL_STATUS_STRIDE, 16);
         dec_zero = sizeof(Ctrl) + round_up(off_blocks * 8, 16);
         const size_t dec_bytes = dec_zero + round_up((dec_tiles + 1) * 8, 16);
         bytes = enc_zero > dec_bytes ? enc_zero : dec_bytes;
@@ -660,7 +660,7 @@ extern "C" int flrl_fl_encode_device(const uint8_t *d_in, size_t n, uint8_t *d_b
         return set_error(FLRL_E_ARG, "flrl_fl_encode_device: input too large");
     FLRL_HIP(scratch_reset(d_scratch, L.enc_zero, s));
     Ctrl *ctrl = static_cast<Ctrl *>(d_scratch);
-    uint64_t *status = reinterpret_cast<uint64_t *>(ctrl + 1);
+    uint64_t *status = reinterpret_cast<uint64_t *>(static_cast<char *>(d_scratch) + FLRL_FL_STATUS_OFF);
     const size_t resident = (size_t)cu_count();
     const uint32_t grid = (uint32_t)(L.enc_tiles < resident ? L.enc_tiles : resident);
     kernel_timing_begin(s);

@@ -52,6 +52,9 @@ constexpr int kRlLaneBytes = 64;                    // contiguous bytes per lane
 constexpr int kRlSub = 32768 / (64 * kRlLaneBytes); // sub-chunks per wave chunk (one look-back per tile)
 constexpr int kRlTileBytes = kRlLaneBytes * kRlThreads * kRlSub;  // 128 KiB: 4 waves x 32 KiB
 constexpr int kRlLookG = FLRL_RL_LOOKG;  // look-back granules per lane (window 64 G tiles)
+constexpr int kRlLookL = FLRL_RL_LOOKL;  // look-back lanes polled per window
+constexpr int kRlStatusStride = FLRL_RL_STATUS_STRIDE;  // status granules per tile
+constexpr size_t kRlStatusOff = FLRL_RL_STATUS_OFF;    // status array offset in the scratch
 constexpr int kRlStageBytes = FLRL_RL_STAGE;  // LDS run staging per workgroup
 // 5 workgroups of 4 waves per CU (LDS-bound: < 32 KiB each): 5 waves per SIMD,
 // so at most 96 VGPRs
@@ -183,17 +186,19 @@ __device__ __forceinline__ uint64_t sm_compose(uint64_t a, uint64_t b)
 // shuffle tree), this tile's P is published and the Const state at the tile
 // start returned. Composed window maps span <= 64*G tiles of <= 128 KiB, within
 // the 26-bit packed fields; across windows the accumulator is kept unpacked.
+template <int S>
 __device__ __forceinline__ void publish_seg(uint64_t *status, uint32_t tile, uint64_t map)
 {
     if ((threadIdx.x & (kWave - 1)) == 0)
-        granule_store(&status[tile], tile == 0 ? (kFlagP | sm_compose(sm_const(0, 0), map))
+        granule_store(&status[(size_t)tile * S], tile == 0 ? (kFlagP | sm_compose(sm_const(0, 0), map))
                                                : (kFlagA | map));
 }
 
-template <int G>
+template <int G, int L, int S>
 __device__ __forceinline__ uint64_t lookback_seg(uint64_t *status, uint32_t tile, uint64_t map,
                                                  Ctrl *ctrl)
 {
+    static_assert(L >= 1 && L <= kWave && (G == 1 || L == kWave), "window of L lanes x G granules");
     const int lane = threadIdx.x & (kWave - 1);
     const uint64_t kPay = (1ull << 62) - 1;
     if (tile == 0)
@@ -213,7 +218,9 @@ __device__ __forceinline__ uint64_t lookback_seg(uint64_t *status, uint32_t tile
         for (;;) {
 #pragma unroll
             for (int k = 0; k < G; ++k)
-                s[k] = idx - k >= 0 ? granule_load(&status[idx - k]) : (kFlagP | sm_const(0, 0));
+                s[k] = lane >= L     ? (kFlagA | sm_nonat(0))
+                       : idx - k >= 0 ? granule_load(&status[(idx - k) * S])
+                                      : (kFlagP | sm_const(0, 0));
             // lane-local: compose from the lane's nearest P (or its oldest
             // granule) forward; ready if nothing up to that P is unpublished
             has_p = false;
@@ -272,7 +279,7 @@ __device__ __forceinline__ uint64_t lookback_seg(uint64_t *status, uint32_t tile
             }
             res = sm_const(H, c);
             if (lane == 0)
-                granule_store(&status[tile], kFlagP | sm_compose(res, map));
+                granule_store(&status[(size_t)tile * S], kFlagP | sm_compose(res, map));
             FLRL_RL_LB_STAT(tile, spins, rounds);
             return res;
         }
@@ -290,7 +297,7 @@ __device__ __forceinline__ uint64_t lookback_seg(uint64_t *status, uint32_t tile
         } else {
             acc_a = sm_a(win) + acc_a;
         }
-        j -= (int64_t)kWave * G;
+        j -= (int64_t)L * G;
     }
 }
 
@@ -914,9 +921,9 @@ __global__ __launch_bounds__(T, kRlWavesPerSimd) void rl_encode_wave_kernel(  //
 #pragma unroll
         for (int v = 1; v < W; ++v)
             tmap = sm_compose(tmap, s_map[v]);
-        publish_seg(status, tile, tmap);
+        publish_seg<kRlStatusStride>(status, tile, tmap);
         FLRL_RL_TRACE(tile, 2);
-        uint64_t st = lookback_seg<kRlLookG>(status, tile, tmap, ctrl);
+        uint64_t st = lookback_seg<kRlLookG, kRlLookL, kRlStatusStride>(status, tile, tmap, ctrl);
         FLRL_RL_TRACE(tile, 3);
         if (V.lane == 0) {
 #pragma unroll
@@ -1759,8 +1766,8 @@ struct RlEncLayout {
         tiles = div_up(n, (size_t)kRlTileBytes);
         if (!three) {
             sblocks = 0;
-            o_status = sizeof(Ctrl);
-            zero = sizeof(Ctrl) + round_up(tiles * 8, 16);  // ticket, error, status granules
+            o_status = kRlStatusOff;
+            zero = kRlStatusOff + round_up(tiles * 8 * kRlStatusStride, 16);  // ticket, error, status
             o_tmap = o_tstate = o_bagg = o_bpre = o_sums = o_stage = bytes = zero;
             return;
         }

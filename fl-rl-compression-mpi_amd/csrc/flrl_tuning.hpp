@@ -11,7 +11,9 @@
 
 #if !defined(FLRL_TUNING_BUILD) &&                                                                  \
     (defined(FLRL_RL_TRACE) || defined(FLRL_RL_LB_STAT) || defined(FLRL_FL_TRACE) ||                \
-     defined(FLRL_RL_THREADS) || defined(FLRL_RL_LOOKG) ||                   \
+     defined(FLRL_RL_THREADS) || defined(FLRL_RL_LOOKG) || defined(FLRL_FL_LOOKG) || defined(FLRL_FL_LOOKL) ||\
+     defined(FLRL_FL_STATUS_STRIDE) || defined(FLRL_FL_STATUS_OFF) || defined(FLRL_RL_LOOKL) ||\
+     defined(FLRL_RL_STATUS_STRIDE) || defined(FLRL_RL_STATUS_OFF) ||\
      defined(FLRL_RL_STAGE) || defined(FLRL_RL_WPS) || defined(FLRL_RD_NARROW_MEAN) || defined(FLRL_RL_RO_MAXB) ||          \
      defined(FLRL_RD_UNROLL) || defined(FLRL_HOST_WORKERS) || defined(FLRL_HOST_CHUNK) ||                \
      defined(FLRL_HOST_DIRECT) || defined(FLRL_HOST_THP) || defined(FLRL_RL_WD64_MEAN) || defined(FLRL_RL_DENSE_MEAN))
@@ -39,8 +41,29 @@
 #ifndef FLRL_RL_THREADS
 #define FLRL_RL_THREADS 256  // 4 waves (LB 64: 94 VGPRs, < 32 KiB LDS, 5 per CU)
 #endif
+#ifndef FLRL_FL_LOOKG
+#define FLRL_FL_LOOKG 1  // FL encode look-back granules per lane (window 64 G tiles)
+#endif
+#ifndef FLRL_FL_LOOKL
+#define FLRL_FL_LOOKL 32  // FL encode look-back lanes polled per window (G must be 1 below 64)
+#endif
+#ifndef FLRL_FL_STATUS_STRIDE
+#define FLRL_FL_STATUS_STRIDE 16  // FL encode status: one 128-B line per tile (polls spread over lines)
+#endif
+#ifndef FLRL_FL_STATUS_OFF
+#define FLRL_FL_STATUS_OFF 256  // FL encode status array offset (Ctrl with the ticket on its own lines)
+#endif
 #ifndef FLRL_RL_LOOKG
 #define FLRL_RL_LOOKG 1  // look-back granules per lane (window 64 G tiles)
+#endif
+#ifndef FLRL_RL_LOOKL
+#define FLRL_RL_LOOKL 64  // RL encode look-back lanes polled per window (G must be 1 below 64)
+#endif
+#ifndef FLRL_RL_STATUS_STRIDE
+#define FLRL_RL_STATUS_STRIDE 16  // RL encode status: one 128-B line per tile (polls spread over lines)
+#endif
+#ifndef FLRL_RL_STATUS_OFF
+#define FLRL_RL_STATUS_OFF 256  // RL encode status array offset (Ctrl with the ticket on its own lines)
 #endif
 #ifndef FLRL_RL_STAGE
 #define FLRL_RL_STAGE 15360  // LDS run staging per workgroup (bytes)

@@ -70,7 +70,7 @@ def main():
     s = torch.cuda.current_stream().cuda_stream
     def roomy(d):
         """scratch with room for builds whose scratch layout is larger"""
-        d.scratch_bytes = 2 * d.scratch_bytes + (1 << 20)
+        d.scratch_bytes = 2 * d.scratch_bytes + (1 << 24)
         d.scratch = torch.empty(d.scratch_bytes, dtype=torch.uint8, device="cuda")
 
     if a.op.startswith("fl"):
