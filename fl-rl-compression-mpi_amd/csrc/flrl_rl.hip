@@ -1294,8 +1294,9 @@ __global__ __launch_bounds__(kRoThreads, 4) void rl_offsets_kernel(  // 4 workgr
 // indices tile-local); pfx = the byte-prefix popcount table; before = runs
 // starting before the window. The run of the chunk's first byte is (runs
 // before it) + (its start bit) - 1; byte i takes run r + k_i (k_i = start bits
-// in bytes 1..i, <= 15), gathered from the 16 values from run r on with byte
-// permutes.
+// in bytes 1..i), gathered with byte permutes. (Gathering from the 16 values
+// from run r on took three permutes per dword; two 8-value windows take one:
+// VALU instructions -25 %, 1 GiB runs32 kernel -2..6 %.)
 __device__ __forceinline__ u32x4 rd_chunk(const uint32_t *bm, const uint32_t *pre, const uint32_t *v32,
                                           const uint64_t *pfx, uint32_t q, uint32_t before)
 {
@@ -1310,27 +1311,25 @@ __device__ __forceinline__ u32x4 rd_chunk(const uint32_t *bm, const uint32_t *pr
     }
     // (no separate path for chunks without an inner start, m1 = 0: a wave
     // almost always holds both kinds, so it would run both; -2 %)
+    // k_i <= i and k_(i+1) - k_i <= 1, so each 8-byte half needs only the 8
+    // values from its own first run on: bytes 0-7 take values r + k_i (k_i <=
+    // 7), bytes 8-15 values r8 + (k_i - k_8) with r8 = r + k_8 -- one byte
+    // permute per output dword, selectors straight from the table
     const uint32_t a = (uint32_t)r >> 2, sh = (uint32_t)r & 3u;
-    const uint32_t d0 = v32[a], d1 = v32[a + 1], d2 = v32[a + 2], d3 = v32[a + 3], d4 = v32[a + 4];
+    const uint32_t d0 = v32[a], d1 = v32[a + 1], d2 = v32[a + 2];
+    const uint32_t r8 = (uint32_t)r + (uint32_t)__popc(m1 & 0x1FFu);
+    const uint32_t a8 = r8 >> 2, sh8 = r8 & 3u;
+    const uint32_t e0 = v32[a8], e1 = v32[a8 + 1], e2 = v32[a8 + 2];
+    const uint64_t klo = pfx[m1 & 0xFFu], khi = pfx[(m1 >> 8) & 0xFEu];
     const uint32_t w0 = __builtin_amdgcn_alignbyte(d1, d0, sh);
     const uint32_t w1 = __builtin_amdgcn_alignbyte(d2, d1, sh);
-    const uint32_t w2 = __builtin_amdgcn_alignbyte(d3, d2, sh);
-    const uint32_t w3 = __builtin_amdgcn_alignbyte(d4, d3, sh);
-    // k_i as bytes: pfx[x] byte i = popcount of x's bits 0..i (a table: no
-    // 64-bit multiplies); the high half adds the low byte's total (no
-    // multiplies: v_mul_lo_u32 is a quarter-rate instruction)
-    const uint64_t klo = pfx[m1 & 0xFFu], kh = pfx[m1 >> 8];
-    const uint32_t plo = __builtin_amdgcn_perm(0u, (uint32_t)__popc(m1 & 0xFFu), 0u);
-    const uint32_t k4[4] = {(uint32_t)klo, (uint32_t)(klo >> 32), (uint32_t)kh + plo, (uint32_t)(kh >> 32) + plo};
+    const uint32_t u0 = __builtin_amdgcn_alignbyte(e1, e0, sh8);
+    const uint32_t u1 = __builtin_amdgcn_alignbyte(e2, e1, sh8);
     u32x4 o;
-#pragma unroll
-    for (int d = 0; d < 4; ++d) {
-        const uint32_t sel = k4[d];
-        const uint32_t lo8 = __builtin_amdgcn_perm(w1, w0, sel & 0x07070707u);
-        const uint32_t hi8 = __builtin_amdgcn_perm(w3, w2, sel & 0x07070707u);
-        // byte i from hi8 (selector 4 + i) where k_i >= 8, else from lo8 (i)
-        o[d] = __builtin_amdgcn_perm(hi8, lo8, ((sel >> 1) & 0x04040404u) | 0x03020100u);
-    }
+    o[0] = __builtin_amdgcn_perm(w1, w0, (uint32_t)klo);
+    o[1] = __builtin_amdgcn_perm(w1, w0, (uint32_t)(klo >> 32));
+    o[2] = __builtin_amdgcn_perm(u1, u0, (uint32_t)khi);
+    o[3] = __builtin_amdgcn_perm(u1, u0, (uint32_t)(khi >> 32));
     return o;
 }
 
@@ -1352,12 +1351,17 @@ __device__ __forceinline__ u32x4 rd_chunk(const uint32_t *bm, const uint32_t *pr
 // Measured against the LDS-window memset decode (scripts/ab_rl_decode.py, one
 // process, decode call incl. offsets pre-pass): runs32 0.338 -> 0.290 ms,
 // longruns 0.313 -> 0.272, random bytes 1.74 -> 1.24, lo4 1.79 -> 1.29.
+// s_st index of run j: rows of 16 runs rotated by the row number, so the
+// block scan's writes (thread t: runs 16t .. 16t + 15, one per instruction)
+// spread over 16 banks instead of two; the marks' reads (consecutive j) stay
+// conflict-free
+__device__ __forceinline__ uint32_t rd_swz(uint32_t j) { return j ^ ((j >> 4) & 15u); }
 constexpr int kRkWindow = 65536;            // output bytes per window
 constexpr int kRkWords = kRkWindow / 32;    // bitmap words per window
 constexpr int kRkDense = 32768;             // tiles with at most this much output: per-thread memsets
 
 template <int T>
-__global__ __launch_bounds__(T) void rl_decode_kernel(
+__global__ __launch_bounds__(T, 4) void rl_decode_kernel(  // 2nd: waves per SIMD (2 or 4 WG per CU)
     const uint8_t *__restrict__ counts, const uint8_t *__restrict__ values, uint64_t runs,
     uint8_t *__restrict__ out, uint64_t n, const uint64_t *__restrict__ tile_base, uint64_t ntiles)
 {
@@ -1469,11 +1473,11 @@ __global__ __launch_bounds__(T) void rl_decode_kernel(
                 uint32_t run = before + inc - sum;  // tile-local start of this thread's first run
 #pragma unroll
                 for (int i = 0; i < RPT; ++i) {
-                    s_st[tid * RPT + i] = run;
+                    s_st[rd_swz(tid * RPT + i)] = run;
                     run += c[i];
                 }
                 if (tid == T - 1)
-                    s_st[kRdRuns] = run;
+                    s_st[rd_swz(kRdRuns)] = run;
             }
             const uint32_t nr = (uint32_t)(runs - tile * kRdRuns < (uint64_t)kRdRuns ? runs - tile * kRdRuns
                                                                                       : kRdRuns);
@@ -1495,7 +1499,7 @@ __global__ __launch_bounds__(T) void rl_decode_kernel(
                         const uint32_t j = (uint32_t)(k * T + tid);
                         if (j >= nr)
                             break;
-                        const uint32_t x0 = s_st[j], x1 = s_st[j + 1];
+                        const uint32_t x0 = s_st[rd_swz(j)], x1 = s_st[rd_swz(j + 1)];
                         const int32_t x = tb + (int32_t)x0;
                         if (x >= kRkWindow)
                             break;

@@ -86,10 +86,11 @@
 #ifndef FLRL_RL_RO_MAXB
 #define FLRL_RL_RO_MAXB 256
 #endif
-// Block decode chunk loop unroll: 8 (a 512-thread window in full): runs32
-// -3 %, runs of 1..32 -4 % vs 4.
+// Block decode chunk loop unroll: 4. (8 was 3-4 % faster with the
+// three-permute chunk assembly; with the two-window assembly it needs more
+// than the 128 VGPRs of 4 waves per SIMD and spills: 256 MiB runs32 +11 %.)
 #ifndef FLRL_RD_UNROLL
-#define FLRL_RD_UNROLL 8
+#define FLRL_RD_UNROLL 4
 #endif
 // Wave decode: 64 runs per lane up to this mean run length, and the wave
 // decode at all up to FLRL_RL_DENSE_MEAN.

@@ -8,7 +8,7 @@ export TMPDIR=/tmp
 OP=$1; KIND=$2; LIB=${3:-fl-rl-compression-mpi_amd/lib/libflrl.so}; TAG=${4:-$OP_$KIND}
 OUT=gpurun_out/pmc_ab/$TAG
 rm -rf "$OUT"; mkdir -p "$OUT"
-CMD=(python3 scripts/ab_libs.py --op "$OP" --libs "$LIB" --kind "$KIND" --reps 4)
+CMD=(python3 scripts/ab_libs.py --op "$OP" --libs "$LIB" --kind "$KIND" --reps 4 ${BYTES:+--bytes $BYTES})
 timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- "${CMD[@]}" > "$OUT/trace.log" 2>&1 || [ -n "$ALLOWFAIL" ] || { echo "trace failed"; tail -5 "$OUT/trace.log"; exit 1; }
 [ -n "$NOPMC" ] && { python3 scripts/pmc_summary.py "$OUT"; exit 0; }
 i=0
