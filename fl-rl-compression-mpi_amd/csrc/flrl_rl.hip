@@ -51,7 +51,6 @@ constexpr int kRlThreads = FLRL_RL_THREADS;         // encode workgroup: 4 waves
 constexpr int kRlLaneBytes = 64;                    // contiguous bytes per lane (a u64 head mask)
 constexpr int kRlSub = 32768 / (64 * kRlLaneBytes); // sub-chunks per wave chunk (one look-back per tile)
 constexpr int kRlTileBytes = kRlLaneBytes * kRlThreads * kRlSub;  // 128 KiB: 4 waves x 32 KiB
-constexpr int kRlLookG = FLRL_RL_LOOKG;  // look-back granules per lane (window 64 G tiles)
 constexpr int kRlLookL = FLRL_RL_LOOKL;  // look-back lanes polled per window
 constexpr int kRlStatusStride = FLRL_RL_STATUS_STRIDE;  // status granules per tile
 constexpr size_t kRlStatusOff = FLRL_RL_STATUS_OFF;    // status array offset in the scratch
@@ -194,11 +193,20 @@ __device__ __forceinline__ void publish_seg(uint64_t *status, uint32_t tile, uin
                                                : (kFlagA | map));
 }
 
-template <int G, int L, int S>
+// help(t): tile t's map computed by this wave from the input (decoupled
+// fallback). Tiles are numbered by workgroup index, not by a ticket: a ticket
+// per workgroup start cost 10-23 % (its atomic round trip on one counter heads
+// every tile's life). Within one launch the dispatcher starts workgroups in
+// index order on each XCD, so a predecessor that has not published is running
+// or about to start; but with other work on the GPU (another look-back kernel
+// on a second stream holding the CUs) it may not start for a long time, so a
+// slot unpublished for kHelpTicks is computed here instead of waited for.
+constexpr uint64_t kHelpTicks = FLRL_RL_HELP_TICKS;  // s_memrealtime ticks (100 MHz)
+template <int L, int S, class Help>
 __device__ __forceinline__ uint64_t lookback_seg(uint64_t *status, uint32_t tile, uint64_t map,
-                                                 Ctrl *ctrl)
+                                                 Ctrl *ctrl, Help &&help)
 {
-    static_assert(L >= 1 && L <= kWave && (G == 1 || L == kWave), "window of L lanes x G granules");
+    static_assert(L >= 1 && L <= kWave, "window of L lanes");
     const int lane = threadIdx.x & (kWave - 1);
     const uint64_t kPay = (1ull << 62) - 1;
     if (tile == 0)
@@ -211,36 +219,24 @@ __device__ __forceinline__ uint64_t lookback_seg(uint64_t *status, uint32_t tile
     uint32_t spins = 0, rounds = 0;
     for (;;) {
         ++rounds;
-        const int64_t idx = j - (int64_t)lane * G;
-        uint64_t s[G];
+        const int64_t idx = j - (int64_t)lane;
+        uint64_t ov = 0;  // this lane's slot as computed by help (0: none)
+        uint64_t t0 = 0;
+        bool helping = false;
         uint64_t m;
         bool has_p;
         for (;;) {
-#pragma unroll
-            for (int k = 0; k < G; ++k)
-                s[k] = lane >= L     ? (kFlagA | sm_nonat(0))
-                       : idx - k >= 0 ? granule_load(&status[(idx - k) * S])
-                                      : (kFlagP | sm_const(0, 0));
-            // lane-local: compose from the lane's nearest P (or its oldest
-            // granule) forward; ready if nothing up to that P is unpublished
-            has_p = false;
-            bool ok = true;
-            m = sm_nonat(0);
-#pragma unroll
-            for (int k = 0; k < G; ++k) {
-                if (!has_p) {
-                    const uint32_t f = (uint32_t)(s[k] >> 62);
-                    ok = ok && f != 0;
-                    if (f == 2) {
-                        has_p = true;
-                        m = sm_compose(sm_const(sm_h(s[k]), sm_c(s[k])), m);
-                    } else {
-                        m = sm_compose(s[k] & kPay, m);
-                    }
-                }
-            }
+            uint64_t s = lane >= L   ? (kFlagA | sm_nonat(0))
+                         : idx >= 0 ? granule_load(&status[idx * S])
+                                    : (kFlagP | sm_const(0, 0));
+            if ((s >> 62) == 0 && ov != 0)
+                s = ov;
+            // ready if nothing up to the window's nearest P is unpublished
+            const uint32_t f = (uint32_t)(s >> 62);
+            has_p = f == 2;
+            m = has_p ? sm_compose(sm_const(sm_h(s), sm_c(s)), sm_nonat(0)) : sm_compose(s & kPay, sm_nonat(0));
             const unsigned long long pm = __ballot(has_p);
-            const unsigned long long bad = __ballot(!ok);
+            const unsigned long long bad = __ballot(f == 0);
             const unsigned long long upto = pm ? ((pm & (~pm + 1)) << 1) - 1 : ~0ull;
             if ((bad & upto) == 0)
                 break;
@@ -248,6 +244,20 @@ __device__ __forceinline__ uint64_t lookback_seg(uint64_t *status, uint32_t tile
                 if (lane == 0)
                     raise_error(ctrl, FLRL_E_TIMEOUT);
                 return sm_const(0, 0);
+            }
+            const uint64_t now = __builtin_amdgcn_s_memrealtime();
+            if (!helping) {
+                if (t0 == 0)
+                    t0 = now;
+                else if (now - t0 > kHelpTicks)
+                    helping = true;
+            }
+            if (helping) {  // the oldest unpublished slot the window needs (uniform)
+                const int l = __ffsll(bad & upto) - 1;
+                const uint64_t hm = help((uint32_t)(j - l));
+                if (lane == l)
+                    ov = kFlagA | hm;
+                continue;
             }
             __builtin_amdgcn_s_sleep(1);
         }
@@ -297,7 +307,7 @@ __device__ __forceinline__ uint64_t lookback_seg(uint64_t *status, uint32_t tile
         } else {
             acc_a = sm_a(win) + acc_a;
         }
-        j -= (int64_t)L * G;
+        j -= (int64_t)L;
     }
 }
 
@@ -880,9 +890,69 @@ struct RlWave {
     }
 };
 
-// One tile per workgroup (grid = tiles), in ticket order: stage, publish the
-// tile map, ONE look-back by wave 0 while waves 1-3 wait, emit. Three block
-// barriers per tile (ticket, wave maps, state).
+__device__ __forceinline__ uint64_t dpp64_up(uint64_t v, int step)
+{
+    switch (step) {
+    case 0: return ((uint64_t)dpp_up0<0x111, 0xF>((uint32_t)(v >> 32)) << 32) | dpp_up0<0x111, 0xF>((uint32_t)v);
+    case 1: return ((uint64_t)dpp_up0<0x112, 0xF>((uint32_t)(v >> 32)) << 32) | dpp_up0<0x112, 0xF>((uint32_t)v);
+    case 2: return ((uint64_t)dpp_up0<0x114, 0xF>((uint32_t)(v >> 32)) << 32) | dpp_up0<0x114, 0xF>((uint32_t)v);
+    case 3: return ((uint64_t)dpp_up0<0x118, 0xF>((uint32_t)(v >> 32)) << 32) | dpp_up0<0x118, 0xF>((uint32_t)v);
+    case 4: return ((uint64_t)dpp_up0<0x142, 0xA>((uint32_t)(v >> 32)) << 32) | dpp_up0<0x142, 0xA>((uint32_t)v);
+    default: return ((uint64_t)dpp_up0<0x143, 0xC>((uint32_t)(v >> 32)) << 32) | dpp_up0<0x143, 0xC>((uint32_t)v);
+    }
+}
+__device__ __forceinline__ uint64_t wave_incl_scan_sm(uint64_t m)
+{
+#pragma unroll
+    for (int k = 0; k < 6; ++k)
+        m = sm_compose(dpp64_up(m, k), m);
+    return m;
+}
+
+// The map of tile t from its input, for the look-back's fallback (help): each
+// lane walks its 1/64 of the tile byte by byte with the encoder's state rule
+// (a byte is a head iff it is natural or c == 0; then c = 1, else c = c + 1
+// mod 255) and the lanes' maps are composed across the wave. Few registers, so
+// the hot path keeps its allocation; slow (~tens of microseconds), which the
+// fallback can afford.
+template <int TBT>
+__device__ uint64_t rl_tile_map_slow(const uint8_t *__restrict__ in, uint64_t n, uint32_t t)
+{
+    constexpr uint32_t PER = TBT / kWave;
+    const int lane = threadIdx.x & (kWave - 1);
+    const uint64_t a = (uint64_t)t * TBT + (uint64_t)lane * PER;
+    const uint64_t b = a + PER < n ? a + PER : n;
+    const uint32_t cnt = a < b ? (uint32_t)(b - a) : 0u;
+    const uint8_t *const p = in + a;
+    uint32_t pre = 0, K = 0, c = 0, prev = a > 0 && a < n ? p[-1] : 0u;
+    bool seen = false;
+#pragma unroll 1
+    for (uint32_t i = 0; i < cnt; ++i) {  // byte loads: the fewest registers
+        const uint32_t x = p[i];
+        const bool nat = (a == 0 && i == 0) || x != prev;
+        if (!seen) {
+            if (nat) {
+                seen = true;
+                K = 1;
+                c = 1;
+            } else {
+                ++pre;
+            }
+        } else if (nat || c == 0) {
+            ++K;
+            c = 1;
+        } else {
+            c = c + 1 == 255 ? 0u : c + 1;
+        }
+        prev = x;
+    }
+    const uint64_t m = seen ? sm_nat(pre, K, c) : sm_nonat(cnt);
+    return readlane64(wave_incl_scan_sm(m), kWave - 1);
+}
+
+// One tile per workgroup (grid = tiles, tile = workgroup index): stage,
+// publish the tile map, ONE look-back by wave 0 while waves 1-3 wait, emit.
+// Two block barriers per tile (wave maps, state).
 template <int T, int LB, int SUB>
 __global__ __launch_bounds__(T, kRlWavesPerSimd) void rl_encode_wave_kernel(  // (2nd: waves per SIMD)
     const uint8_t *__restrict__ in, uint64_t n, uint32_t ntiles, uint8_t *__restrict__ counts,
@@ -893,17 +963,13 @@ __global__ __launch_bounds__(T, kRlWavesPerSimd) void rl_encode_wave_kernel(  //
     __shared__ __attribute__((aligned(16))) uint8_t s_lds[Wv::kLdsBytes];
     __shared__ uint64_t s_map[W];
     __shared__ uint64_t s_st[W];
-    __shared__ uint32_t s_ticket;
 
     const int tid = threadIdx.x;
     const int w = tid / kWave;
     const Wv V(in, n, s_lds, w);
-    const uint32_t tile = take_ticket(ctrl, &s_ticket);
-    if (tile >= ntiles) {  // the scratch's ticket was not reset for this launch
-        if (threadIdx.x == 0)
-            raise_error(ctrl, FLRL_E_ARG);
+    const uint32_t tile = blockIdx.x;  // (lookback_seg: why not a ticket)
+    if (tile >= ntiles)
         return;
-    }
     FLRL_RL_TRACE(tile, 0);
     typename Wv::Chunk C;
     {
@@ -923,7 +989,9 @@ __global__ __launch_bounds__(T, kRlWavesPerSimd) void rl_encode_wave_kernel(  //
             tmap = sm_compose(tmap, s_map[v]);
         publish_seg<kRlStatusStride>(status, tile, tmap);
         FLRL_RL_TRACE(tile, 2);
-        uint64_t st = lookback_seg<kRlLookG, kRlLookL, kRlStatusStride>(status, tile, tmap, ctrl);
+        // decoupled fallback: a predecessor tile's map from its input
+        auto help = [&](uint32_t t) -> uint64_t { return rl_tile_map_slow<Wv::TBT>(in, n, t); };
+        uint64_t st = lookback_seg<kRlLookL, kRlStatusStride>(status, tile, tmap, ctrl, help);
         FLRL_RL_TRACE(tile, 3);
         if (V.lane == 0) {
 #pragma unroll
@@ -936,6 +1004,10 @@ __global__ __launch_bounds__(T, kRlWavesPerSimd) void rl_encode_wave_kernel(  //
     __syncthreads();
     V.emit(C, sm_h(s_st[w]), sm_c(s_st[w]), counts, values, runs_out);
     FLRL_RL_TRACE(tile, 4);
+    // a launch counts exactly ntiles: more means the scratch was not reset for
+    // it (its status words were stale too, so the output is not trusted)
+    if (tid == 0 && atomicAdd(&ctrl->ticket, 1u) >= ntiles)
+        raise_error(ctrl, FLRL_E_ARG);
 }
 
 // ---- RL encode in three passes (no look-back wait) ---------------------------
@@ -1013,24 +1085,6 @@ __global__ __launch_bounds__(T, kRlWavesPerSimd) void rl_encode_scan_kernel(cons
 
 // inclusive wave scan of segment maps (oldest first; lanes without a source
 // read 0 = the identity map "no natural head, 0 bytes")
-__device__ __forceinline__ uint64_t dpp64_up(uint64_t v, int step)
-{
-    switch (step) {
-    case 0: return ((uint64_t)dpp_up0<0x111, 0xF>((uint32_t)(v >> 32)) << 32) | dpp_up0<0x111, 0xF>((uint32_t)v);
-    case 1: return ((uint64_t)dpp_up0<0x112, 0xF>((uint32_t)(v >> 32)) << 32) | dpp_up0<0x112, 0xF>((uint32_t)v);
-    case 2: return ((uint64_t)dpp_up0<0x114, 0xF>((uint32_t)(v >> 32)) << 32) | dpp_up0<0x114, 0xF>((uint32_t)v);
-    case 3: return ((uint64_t)dpp_up0<0x118, 0xF>((uint32_t)(v >> 32)) << 32) | dpp_up0<0x118, 0xF>((uint32_t)v);
-    case 4: return ((uint64_t)dpp_up0<0x142, 0xA>((uint32_t)(v >> 32)) << 32) | dpp_up0<0x142, 0xA>((uint32_t)v);
-    default: return ((uint64_t)dpp_up0<0x143, 0xC>((uint32_t)(v >> 32)) << 32) | dpp_up0<0x143, 0xC>((uint32_t)v);
-    }
-}
-__device__ __forceinline__ uint64_t wave_incl_scan_sm(uint64_t m)
-{
-#pragma unroll
-    for (int k = 0; k < 6; ++k)
-        m = sm_compose(dpp64_up(m, k), m);
-    return m;
-}
 
 constexpr int kRsThreads = 256;  // tile maps per state-scan workgroup
 
