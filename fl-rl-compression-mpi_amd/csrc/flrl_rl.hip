@@ -200,11 +200,12 @@ __device__ __forceinline__ void publish_seg(uint64_t *status, uint32_t tile, uin
 // index order on each XCD, so a predecessor that has not published is running
 // or about to start; but with other work on the GPU (another look-back kernel
 // on a second stream holding the CUs) it may not start for a long time, so a
-// slot unpublished for kHelpTicks is computed here instead of waited for.
-constexpr uint64_t kHelpTicks = FLRL_RL_HELP_TICKS;  // s_memrealtime ticks (100 MHz)
+// slot unpublished for help_ticks (s_memrealtime, 100 MHz; kRlHelpTicks unless
+// a test sets it) is computed here instead of waited for.
+constexpr uint64_t kRlHelpTicks = 20000;  // 200 us
 template <int L, int S, class Help>
 __device__ __forceinline__ uint64_t lookback_seg(uint64_t *status, uint32_t tile, uint64_t map,
-                                                 Ctrl *ctrl, Help &&help)
+                                                 Ctrl *ctrl, uint64_t help_ticks, Help &&help)
 {
     static_assert(L >= 1 && L <= kWave, "window of L lanes");
     const int lane = threadIdx.x & (kWave - 1);
@@ -249,7 +250,7 @@ __device__ __forceinline__ uint64_t lookback_seg(uint64_t *status, uint32_t tile
             if (!helping) {
                 if (t0 == 0)
                     t0 = now;
-                else if (now - t0 > kHelpTicks)
+                else if (now - t0 >= help_ticks)
                     helping = true;
             }
             if (helping) {  // the oldest unpublished slot the window needs (uniform)
@@ -956,7 +957,8 @@ __device__ uint64_t rl_tile_map_slow(const uint8_t *__restrict__ in, uint64_t n,
 template <int T, int LB, int SUB>
 __global__ __launch_bounds__(T, kRlWavesPerSimd) void rl_encode_wave_kernel(  // (2nd: waves per SIMD)
     const uint8_t *__restrict__ in, uint64_t n, uint32_t ntiles, uint8_t *__restrict__ counts,
-    uint8_t *__restrict__ values, uint64_t *__restrict__ runs_out, Ctrl *ctrl, uint64_t *status)
+    uint8_t *__restrict__ values, uint64_t *__restrict__ runs_out, Ctrl *ctrl, uint64_t *status,
+    uint64_t help_ticks)
 {
     constexpr int W = T / kWave;
     using Wv = RlWave<LB, SUB, W>;
@@ -991,7 +993,7 @@ __global__ __launch_bounds__(T, kRlWavesPerSimd) void rl_encode_wave_kernel(  //
         FLRL_RL_TRACE(tile, 2);
         // decoupled fallback: a predecessor tile's map from its input
         auto help = [&](uint32_t t) -> uint64_t { return rl_tile_map_slow<Wv::TBT>(in, n, t); };
-        uint64_t st = lookback_seg<kRlLookL, kRlStatusStride>(status, tile, tmap, ctrl, help);
+        uint64_t st = lookback_seg<kRlLookL, kRlStatusStride>(status, tile, tmap, ctrl, help_ticks, help);
         FLRL_RL_TRACE(tile, 3);
         if (V.lane == 0) {
 #pragma unroll
@@ -1814,6 +1816,10 @@ __global__ __launch_bounds__(kWdThreads) void rl_decode_wave_kernel(
     }
 }
 
+// flrl_debug_rl_help_us: the look-back fallback threshold of this thread's
+// RL encode launches, in s_memrealtime ticks (-1: kRlHelpTicks)
+static thread_local int64_t g_rl_help_ticks = -1;
+
 // single pass: [Ctrl][status: tiles] (zeroed); three passes: [Ctrl] (zeroed)
 // [tmap: tiles][tlocal: tiles][bagg: blocks x 32 B][bpre: blocks x 16 B]
 // [sums: tiles x 4 x 48 B][staged runs: tiles x kRlStageBytes]
@@ -1866,6 +1872,14 @@ struct RlDecLayout {
 }  // namespace flrl
 
 using namespace flrl;
+
+extern "C" int flrl_debug_rl_help_us(int microseconds)
+{
+    if (microseconds < -1)
+        return set_error(FLRL_E_ARG, "flrl_debug_rl_help_us: %d < -1", microseconds);
+    g_rl_help_ticks = microseconds < 0 ? -1 : (int64_t)microseconds * 100;  // 100 MHz ticks
+    return FLRL_OK;
+}
 
 static bool rl_form_known(int form) { return form == FLRL_RL_FORM_LOOKBACK || form == FLRL_RL_FORM_THREE_PASS; }
 
@@ -1932,7 +1946,7 @@ extern "C" int flrl_rl_encode_device_form(const uint8_t *d_in, size_t n, uint8_t
         uint64_t *status = reinterpret_cast<uint64_t *>(base + L.o_status);
         hipLaunchKernelGGL((rl_encode_wave_kernel<kRlThreads, kRlLaneBytes, kRlSub>), dim3((uint32_t)L.tiles),
                            dim3(kRlThreads), 0, s, d_in, (uint64_t)n, (uint32_t)L.tiles, d_counts, d_values,
-                           d_runs, ctrl, status);
+                           d_runs, ctrl, status, g_rl_help_ticks < 0 ? kRlHelpTicks : (uint64_t)g_rl_help_ticks);
     }
     kernel_timing_end(s);
     FLRL_HIP(hipGetLastError());

@@ -124,6 +124,69 @@ def test_runs_spanning_many_tiles(passes):
     check(np.concatenate(parts))
 
 
+@pytest.fixture
+def always_help():
+    flrl.debug_rl_help_us(0)
+    yield
+    flrl.debug_rl_help_us(-1)
+
+
+def _fallback_input(case: str) -> np.ndarray:
+    rng = np.random.default_rng(11)
+    if case == "tiles":  # runs of up to 3 tiles: most tiles have no natural head
+        parts, v, total = [], 0, 0
+        while total < 3_000_000:
+            L = int(rng.integers(1, 3 * 131072))
+            parts.append(np.full(L, v, np.uint8))
+            v = (v + 1 + int(rng.integers(0, 200))) % 256
+            total += L
+        return np.concatenate(parts)
+    if case == "late":  # the first natural head in the third tile
+        a = rng.integers(0, 4, size=2_000_000, dtype=np.uint8)
+        a[:2 * 131072 + 77] = 5
+        a[2 * 131072 + 77] = 6
+        return a
+    return oracle.gen(case, 3 * 131072 * 4 + 12345, 23)
+
+
+@pytest.mark.parametrize("case", ["runs32", "longruns", "u8", "zero", "tiles", "late"])
+def test_lookback_fallback_bit_exact(case, always_help):
+    """The decoupled fallback of the RL encode look-back (an unpublished
+    predecessor's map computed from the input; here at the first unpublished
+    poll, so most look-backs of a multi-tile launch take it) gives the oracle's
+    records, and the debug hook restores the default."""
+    from flrl.device import RLDevice
+    a = _fallback_input(case)
+    d = RLDevice(a.size)
+    d.encode(torch.from_numpy(a).cuda())
+    R = d.runs()
+    assert d.error() == 0
+    counts, values = oracle.rl_compress(a)
+    assert R == counts.size
+    assert np.array_equal(d.counts[:R].cpu().numpy(), counts)
+    assert np.array_equal(d.values[:R].cpu().numpy(), values)
+
+
+def test_lookback_fallback_1gib(always_help):
+    from flrl.device import RLDevice
+    n = 1 << 30
+    d = RLDevice(n)
+    x = torch.from_numpy(flrl.gen_host("runs32", n, 42)).cuda()
+    d.encode(x)
+    R = d.runs()
+    assert d.error() == 0
+    flrl.debug_rl_help_us(-1)
+    ref = RLDevice(n)
+    ref.encode(x)
+    assert ref.runs() == R and ref.error() == 0
+    assert torch.equal(d.counts[:R], ref.counts[:R]) and torch.equal(d.values[:R], ref.values[:R])
+
+
+def test_debug_rl_help_us_rejects_below_minus_one():
+    with pytest.raises(flrl.FLRLError):
+        flrl.debug_rl_help_us(-2)
+
+
 @pytest.mark.parametrize("quiet", [1, 32768 - 3, 32768 + 100, 65536 - 3, 98304 + 7, 131072 + 5])
 def test_first_natural_head_late(quiet, passes):
     # no natural head for `quiet` bytes (in the first 32 KiB sub-tile, at and
