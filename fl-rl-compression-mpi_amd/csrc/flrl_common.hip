@@ -146,6 +146,20 @@ extern "C" int flrl_debug_fail_chunk(long long chunk)
     return FLRL_OK;
 }
 
+// flrl_debug_lookback_help_us: the decoupled-fallback threshold of this
+// thread's look-back launches in s_memrealtime ticks (-1: each kernel's default)
+static thread_local int64_t g_help_ticks = -1;
+
+uint64_t flrl::lookback_help_ticks(uint64_t dflt) { return g_help_ticks < 0 ? dflt : (uint64_t)g_help_ticks; }
+
+extern "C" int flrl_debug_lookback_help_us(int microseconds)
+{
+    if (microseconds < -1)
+        return set_error(FLRL_E_ARG, "flrl_debug_lookback_help_us: %d < -1", microseconds);
+    g_help_ticks = microseconds < 0 ? -1 : (int64_t)microseconds * 100;  // 100 MHz ticks
+    return FLRL_OK;
+}
+
 extern "C" int flrl_debug_skip_scratch_resets(int calls)
 {
     if (calls < 0)

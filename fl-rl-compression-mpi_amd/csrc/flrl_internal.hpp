@@ -29,6 +29,10 @@ hipError_t scratch_reset(void *p, size_t bytes, hipStream_t s);
 // ordered, no host sync): errors a device call finds on the host side but
 // reports, like the kernels' own, through flrl_scratch_error.
 hipError_t raise_error_async(void *scratch, int code, hipStream_t s);
+
+// The decoupled-fallback threshold for a look-back launch: `dflt` ticks
+// (s_memrealtime, 100 MHz) unless flrl_debug_lookback_help_us set this thread's.
+uint64_t lookback_help_ticks(uint64_t dflt);
 // flrl_debug_fail_chunk: true when the streamed file paths should fail chunk c.
 bool debug_fail_chunk(size_t c);
 

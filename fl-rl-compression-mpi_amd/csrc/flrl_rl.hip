@@ -201,7 +201,7 @@ __device__ __forceinline__ void publish_seg(uint64_t *status, uint32_t tile, uin
 // or about to start; but with other work on the GPU (another look-back kernel
 // on a second stream holding the CUs) it may not start for a long time, so a
 // slot unpublished for help_ticks (s_memrealtime, 100 MHz; kRlHelpTicks unless
-// a test sets it) is computed here instead of waited for.
+// flrl_debug_lookback_help_us sets it) is computed here instead of waited for.
 constexpr uint64_t kRlHelpTicks = 20000;  // 200 us
 template <int L, int S, class Help>
 __device__ __forceinline__ uint64_t lookback_seg(uint64_t *status, uint32_t tile, uint64_t map,
@@ -1816,10 +1816,6 @@ __global__ __launch_bounds__(kWdThreads) void rl_decode_wave_kernel(
     }
 }
 
-// flrl_debug_rl_help_us: the look-back fallback threshold of this thread's
-// RL encode launches, in s_memrealtime ticks (-1: kRlHelpTicks)
-static thread_local int64_t g_rl_help_ticks = -1;
-
 // single pass: [Ctrl][status: tiles] (zeroed); three passes: [Ctrl] (zeroed)
 // [tmap: tiles][tlocal: tiles][bagg: blocks x 32 B][bpre: blocks x 16 B]
 // [sums: tiles x 4 x 48 B][staged runs: tiles x kRlStageBytes]
@@ -1872,14 +1868,6 @@ struct RlDecLayout {
 }  // namespace flrl
 
 using namespace flrl;
-
-extern "C" int flrl_debug_rl_help_us(int microseconds)
-{
-    if (microseconds < -1)
-        return set_error(FLRL_E_ARG, "flrl_debug_rl_help_us: %d < -1", microseconds);
-    g_rl_help_ticks = microseconds < 0 ? -1 : (int64_t)microseconds * 100;  // 100 MHz ticks
-    return FLRL_OK;
-}
 
 static bool rl_form_known(int form) { return form == FLRL_RL_FORM_LOOKBACK || form == FLRL_RL_FORM_THREE_PASS; }
 
@@ -1946,7 +1934,7 @@ extern "C" int flrl_rl_encode_device_form(const uint8_t *d_in, size_t n, uint8_t
         uint64_t *status = reinterpret_cast<uint64_t *>(base + L.o_status);
         hipLaunchKernelGGL((rl_encode_wave_kernel<kRlThreads, kRlLaneBytes, kRlSub>), dim3((uint32_t)L.tiles),
                            dim3(kRlThreads), 0, s, d_in, (uint64_t)n, (uint32_t)L.tiles, d_counts, d_values,
-                           d_runs, ctrl, status, g_rl_help_ticks < 0 ? kRlHelpTicks : (uint64_t)g_rl_help_ticks);
+                           d_runs, ctrl, status, lookback_help_ticks(kRlHelpTicks));
     }
     kernel_timing_end(s);
     FLRL_HIP(hipGetLastError());

@@ -114,7 +114,7 @@ _sig("flrl_fl_decode_device", ctypes.c_int, _vp, _sz, _vp, _sz, _vp, _sz, _vp, _
 _sig("flrl_scratch_error", ctypes.c_int, _vp, _vp)
 _sig("flrl_time_next_kernel", ctypes.c_int, _vp, _vp)
 _sig("flrl_debug_skip_scratch_resets", ctypes.c_int, ctypes.c_int)
-_sig("flrl_debug_rl_help_us", ctypes.c_int, ctypes.c_int)
+_sig("flrl_debug_lookback_help_us", ctypes.c_int, ctypes.c_int)
 _sig("flrl_debug_fail_chunk", ctypes.c_int, ctypes.c_longlong)
 _sig("flrl_rl_compress", ctypes.c_int, _vp, _sz, ctypes.POINTER(_RLBuf))
 _sig("flrl_rl_decompress", ctypes.c_int, _sz, _vp, _vp, _sz,
@@ -474,10 +474,10 @@ def debug_skip_scratch_resets(calls: int) -> None:
     _check(_lib.flrl_debug_skip_scratch_resets(calls))
 
 
-def debug_rl_help_us(microseconds: int) -> None:
+def debug_lookback_help_us(microseconds: int) -> None:
     """Test hook: RL encode look-backs compute an unpublished predecessor's map
     after `microseconds` (0: immediately) instead of 200 us; -1 restores."""
-    _check(_lib.flrl_debug_rl_help_us(microseconds))
+    _check(_lib.flrl_debug_lookback_help_us(microseconds))
 
 
 def debug_fail_chunk(chunk: int) -> None:

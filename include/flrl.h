@@ -256,13 +256,14 @@ int flrl_time_next_kernel(void *start_event, void *stop_event);
  * 0 cancels. Never needed by callers. */
 int flrl_debug_skip_scratch_resets(int calls);
 
-/* Test hook (no reference counterpart): RL encode look-backs of this thread's
- * later launches compute a predecessor tile's map from the input once it has
- * been unpublished for `microseconds` (0: at the first unpublished poll),
- * instead of after the default 200 us -- the decoupled fallback that keeps the
- * look-back independent of workgroup dispatch order. -1 restores the default.
- * Output is identical either way; never needed by callers. */
-int flrl_debug_rl_help_us(int microseconds);
+/* Test hook (no reference counterpart): the RL encode look-backs of this
+ * thread's later launches compute an unpublished predecessor tile's map
+ * (its aggregate) from the input once it has been
+ * unpublished for `microseconds` (0: at the first unpublished poll) instead of
+ * after the default 200 us -- the decoupled fallback that keeps them
+ * independent of workgroup dispatch order. -1 restores the default. Output is
+ * identical either way; never needed by callers. */
+int flrl_debug_lookback_help_us(int microseconds);
 
 /* Test hook: the streamed file paths (flrl_*_file) fail when a worker reaches
  * chunk (or RL decode block) `chunk`, as a failed read or device call would.

@@ -126,9 +126,9 @@ def test_runs_spanning_many_tiles(passes):
 
 @pytest.fixture
 def always_help():
-    flrl.debug_rl_help_us(0)
+    flrl.debug_lookback_help_us(0)
     yield
-    flrl.debug_rl_help_us(-1)
+    flrl.debug_lookback_help_us(-1)
 
 
 def _fallback_input(case: str) -> np.ndarray:
@@ -153,8 +153,8 @@ def _fallback_input(case: str) -> np.ndarray:
 def test_lookback_fallback_bit_exact(case, always_help):
     """The decoupled fallback of the RL encode look-back (an unpublished
     predecessor's map computed from the input; here at the first unpublished
-    poll, so most look-backs of a multi-tile launch take it) gives the oracle's
-    records, and the debug hook restores the default."""
+    poll, so most look-backs of a multi-tile launch take it) gives the
+    oracle's records, which decode back to the input."""
     from flrl.device import RLDevice
     a = _fallback_input(case)
     d = RLDevice(a.size)
@@ -165,6 +165,9 @@ def test_lookback_fallback_bit_exact(case, always_help):
     assert R == counts.size
     assert np.array_equal(d.counts[:R].cpu().numpy(), counts)
     assert np.array_equal(d.values[:R].cpu().numpy(), values)
+    out = d.decode(R)
+    assert d.error() == 0
+    assert np.array_equal(out[:a.size].cpu().numpy(), a)
 
 
 def test_lookback_fallback_1gib(always_help):
@@ -175,16 +178,16 @@ def test_lookback_fallback_1gib(always_help):
     d.encode(x)
     R = d.runs()
     assert d.error() == 0
-    flrl.debug_rl_help_us(-1)
+    flrl.debug_lookback_help_us(-1)
     ref = RLDevice(n)
     ref.encode(x)
     assert ref.runs() == R and ref.error() == 0
     assert torch.equal(d.counts[:R], ref.counts[:R]) and torch.equal(d.values[:R], ref.values[:R])
 
 
-def test_debug_rl_help_us_rejects_below_minus_one():
+def test_debug_lookback_help_us_rejects_below_minus_one():
     with pytest.raises(flrl.FLRLError):
-        flrl.debug_rl_help_us(-2)
+        flrl.debug_lookback_help_us(-2)
 
 
 @pytest.mark.parametrize("quiet", [1, 32768 - 3, 32768 + 100, 65536 - 3, 98304 + 7, 131072 + 5])
