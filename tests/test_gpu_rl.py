@@ -185,6 +185,35 @@ def test_lookback_fallback_1gib(always_help):
     assert torch.equal(d.counts[:R], ref.counts[:R]) and torch.equal(d.values[:R], ref.values[:R])
 
 
+def test_concurrent_large_encodes():
+    """Two RL encodes whose grids exceed the GPU (3072 tiles each, 1280
+    resident) on two streams at once: their workgroups interleave on the CUs,
+    so a tile's predecessor may wait behind the other launch (the look-back's
+    fallback covers that); outputs must equal the serial ones."""
+    from flrl.device import RLDevice, gen
+    n = 384 << 20
+    xs = [torch.from_numpy(flrl.gen_host("runs32", n, 5)).cuda(), gen("lo4", n, 6)]
+    ds = [RLDevice(n), RLDevice(n)]
+    ref = []
+    for d, x in zip(ds, xs):
+        d.encode(x)
+        R = d.runs()
+        assert d.error() == 0
+        ref.append((R, d.counts[:R].clone(), d.values[:R].clone()))
+    torch.cuda.synchronize()
+    streams = [torch.cuda.Stream() for _ in range(2)]
+    for rep in range(3):
+        for d in ds:
+            d.counts.zero_()
+        torch.cuda.synchronize()
+        for d, x, st in zip(ds, xs, streams):
+            d.encode(x, stream=st)
+        torch.cuda.synchronize()
+        for i, (d, (R, c0, v0)) in enumerate(zip(ds, ref)):
+            assert d.error() == 0 and d.runs() == R, (rep, i)
+            assert torch.equal(d.counts[:R], c0) and torch.equal(d.values[:R], v0), (rep, i)
+
+
 def test_debug_lookback_help_us_rejects_below_minus_one():
     with pytest.raises(flrl.FLRLError):
         flrl.debug_lookback_help_us(-2)
