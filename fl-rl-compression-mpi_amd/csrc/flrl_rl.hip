@@ -921,16 +921,14 @@ __device__ uint64_t rl_tile_map_slow(const uint8_t *__restrict__ in, uint64_t n,
 {
     constexpr uint32_t PER = TBT / kWave;
     const int lane = threadIdx.x & (kWave - 1);
-    const uint64_t a = (uint64_t)t * TBT + (uint64_t)lane * PER;
+    const uint64_t a = (uint64_t)t * TBT + (uint64_t)lane * PER;  // 4-byte aligned
     const uint64_t b = a + PER < n ? a + PER : n;
     const uint32_t cnt = a < b ? (uint32_t)(b - a) : 0u;
     const uint8_t *const p = in + a;
     uint32_t pre = 0, K = 0, c = 0, prev = a > 0 && a < n ? p[-1] : 0u;
     bool seen = false;
-#pragma unroll 1
-    for (uint32_t i = 0; i < cnt; ++i) {  // byte loads: the fewest registers
-        const uint32_t x = p[i];
-        const bool nat = (a == 0 && i == 0) || x != prev;
+    auto step = [&](uint32_t x, bool first_of_input) {
+        const bool nat = first_of_input || x != prev;
         if (!seen) {
             if (nat) {
                 seen = true;
@@ -946,7 +944,24 @@ __device__ uint64_t rl_tile_map_slow(const uint8_t *__restrict__ in, uint64_t n,
             c = c + 1 == 255 ? 0u : c + 1;
         }
         prev = x;
+    };
+    // whole words with the next one in flight (few registers: the hot path
+    // keeps its allocation), then the last bytes
+    const uint32_t nw = cnt / 4;
+    const uint32_t *const p32 = reinterpret_cast<const uint32_t *>(p);
+    uint32_t w = nw ? p32[0] : 0u;
+#pragma unroll 1
+    for (uint32_t i = 0; i < nw; ++i) {
+        const uint32_t cur = w;
+        if (i + 1 < nw)
+            w = p32[i + 1];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            step((cur >> (8 * k)) & 0xFFu, a == 0 && i == 0 && k == 0);
     }
+#pragma unroll 1
+    for (uint32_t i = 4 * nw; i < cnt; ++i)
+        step(p[i], a == 0 && i == 0);
     const uint64_t m = seen ? sm_nat(pre, K, c) : sm_nonat(cnt);
     return readlane64(wave_incl_scan_sm(m), kWave - 1);
 }
