@@ -73,6 +73,22 @@ hipError_t zero_async(void *p, size_t bytes, hipStream_t s)
     return hipGetLastError();
 }
 
+// [p, p + 16 head16) and the 8-byte words at p + 16 head16 + k stride (k <
+// count): a Ctrl plus look-back status words that sit one per cache line
+// (only the words are ever read, so the lines' other bytes stay as they are)
+__global__ __launch_bounds__(kThreads) void zero_strided_kernel(uint8_t *p, uint32_t head16, uint64_t count,
+                                                                 uint32_t stride)
+{
+    const uint64_t total = head16 + count;
+    for (uint64_t i = (uint64_t)blockIdx.x * kThreads + threadIdx.x; i < total;
+         i += (uint64_t)gridDim.x * kThreads) {
+        if (i < head16)
+            *reinterpret_cast<u32x4 *>(p + 16 * i) = u32x4{0u, 0u, 0u, 0u};
+        else
+            *reinterpret_cast<uint64_t *>(p + 16ull * head16 + (i - head16) * stride) = 0;
+    }
+}
+
 __global__ void raise_error_kernel(Ctrl *ctrl, uint32_t code)
 {
     raise_error(ctrl, code);
@@ -93,6 +109,19 @@ hipError_t scratch_reset(void *p, size_t bytes, hipStream_t s)
         return hipSuccess;
     }
     return zero_async(p, bytes, s);
+}
+
+hipError_t scratch_reset_strided(void *p, size_t head_bytes, size_t count, size_t stride, hipStream_t s)
+{
+    if (g_skip_resets > 0) {
+        --g_skip_resets;
+        return hipSuccess;
+    }
+    const size_t total = head_bytes / 16 + count;
+    const size_t blocks = div_up(total, (size_t)kThreads);
+    hipLaunchKernelGGL(zero_strided_kernel, dim3((uint32_t)(blocks < 1024 ? blocks : 1024)), dim3(kThreads), 0, s,
+                       static_cast<uint8_t *>(p), (uint32_t)(head_bytes / 16), (uint64_t)count, (uint32_t)stride);
+    return hipGetLastError();
 }
 
 // splitmix64 draw number w+1 from `seed` (counter form of SURVEY.md §8(d)).

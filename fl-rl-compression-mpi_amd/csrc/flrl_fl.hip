@@ -664,7 +664,8 @@ extern "C" int flrl_fl_encode_device(const uint8_t *d_in, size_t n, uint8_t *d_b
         return set_error(FLRL_E_ARG, "flrl_fl_encode_device: buffers must be 16-byte aligned");
     if (L.enc_tiles > 0xFFFFFFFFull)
         return set_error(FLRL_E_ARG, "flrl_fl_encode_device: input too large");
-    FLRL_HIP(scratch_reset(d_scratch, L.enc_zero, s));
+    static_assert(FLRL_FL_STATUS_OFF % 16 == 0 && FLRL_FL_STATUS_OFF >= sizeof(Ctrl), "Ctrl area");
+    FLRL_HIP(scratch_reset_strided(d_scratch, FLRL_FL_STATUS_OFF, L.enc_tiles, 8 * FLRL_FL_STATUS_STRIDE, s));
     Ctrl *ctrl = static_cast<Ctrl *>(d_scratch);
     uint64_t *status = reinterpret_cast<uint64_t *>(static_cast<char *>(d_scratch) + FLRL_FL_STATUS_OFF);
     const size_t resident = (size_t)cu_count();

@@ -25,6 +25,9 @@ hipError_t zero_async(void *p, size_t bytes, hipStream_t s);
 // call: zero_async unless flrl_debug_skip_scratch_resets asked this thread to
 // skip it (tests of the kernels' stale-ticket checks).
 hipError_t scratch_reset(void *p, size_t bytes, hipStream_t s);
+// As scratch_reset for a Ctrl area of head_bytes (a multiple of 16) followed by
+// `count` 8-byte status words `stride` bytes apart: only those words are zeroed.
+hipError_t scratch_reset_strided(void *p, size_t head_bytes, size_t count, size_t stride, hipStream_t s);
 // Raise FLRL_E_* `code` in the scratch's error word from stream s (stream
 // ordered, no host sync): errors a device call finds on the host side but
 // reports, like the kernels' own, through flrl_scratch_error.

@@ -1917,7 +1917,12 @@ extern "C" int flrl_rl_encode_device_form(const uint8_t *d_in, size_t n, uint8_t
                          scratch_bytes, L.bytes);
     if (!aligned16(d_scratch))
         return set_error(FLRL_E_ARG, "flrl_rl_encode_device: scratch not 16-byte aligned");
-    FLRL_HIP(scratch_reset(d_scratch, L.zero, s));
+    if (three) {
+        FLRL_HIP(scratch_reset(d_scratch, L.zero, s));
+    } else {
+        static_assert(kRlStatusOff % 16 == 0 && kRlStatusOff >= sizeof(Ctrl), "Ctrl area");
+        FLRL_HIP(scratch_reset_strided(d_scratch, kRlStatusOff, L.tiles, 8 * kRlStatusStride, s));
+    }
     if (n == 0) {
         FLRL_HIP(zero_async(d_runs, sizeof(uint64_t), s));
         return FLRL_OK;
