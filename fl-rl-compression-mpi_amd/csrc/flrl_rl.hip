@@ -1434,7 +1434,8 @@ constexpr int kRkDense = 32768;             // tiles with at most this much outp
 template <int T>
 __global__ __launch_bounds__(T, 4) void rl_decode_kernel(  // 2nd: waves per SIMD (2 or 4 WG per CU)
     const uint8_t *__restrict__ counts, const uint8_t *__restrict__ values, uint64_t runs,
-    uint8_t *__restrict__ out, uint64_t n, const uint64_t *__restrict__ tile_base, uint64_t ntiles)
+    uint8_t *__restrict__ out, uint64_t n, const uint64_t *__restrict__ tile_base, uint64_t ntiles,
+    Ctrl *ctrl, uint32_t ticket0, bool tickets)
 {
     constexpr int kRdRuns = 16 * T;  // runs per tile
     constexpr int RPT = kRdRuns / T;        // runs per thread
@@ -1461,6 +1462,15 @@ __global__ __launch_bounds__(T, 4) void rl_decode_kernel(  // 2nd: waves per SIM
     uint64_t tile = blockIdx.x;
     if (tile >= ntiles)
         return;
+    // tickets: later tiles by ticket, taken one tile ahead (the pre-pass took
+    // tickets 0..ticket0-1), so the workgroups move through the output together
+    // instead of drifting apart grid-stride (runs32: 1 GiB -3.5 %, 4 GiB
+    // -10 %; with two tiles per workgroup, 256 MiB, +14 %: the host asks for
+    // them from eight tiles per workgroup on)
+    __shared__ uint32_t s_tk[2];
+    if (tickets && threadIdx.x == 0)
+        s_tk[0] = atomicAdd(&ctrl->ticket, 1u) - ticket0 + gridDim.x;
+    uint32_t tslot = 1;
     if (tid < 256) {
         static_assert(T >= 256, "one table entry per thread");
         uint64_t e = 0;
@@ -1479,8 +1489,14 @@ __global__ __launch_bounds__(T, 4) void rl_decode_kernel(  // 2nd: waves per SIM
     // of the tile would also wait for that HBM round trip.
     uint64_t tbv = tile_base[tile + (lane & 1)];
     for (;;) {
-        const uint64_t next = tile + gridDim.x;
-        __syncthreads();  // the previous tile's LDS readers are done
+        __syncthreads();  // the previous tile's LDS readers are done; s_tk written
+        uint64_t next = tile + gridDim.x;
+        if (tickets) {
+            next = s_tk[tslot ^ 1u];
+            if (threadIdx.x == 0)
+                s_tk[tslot] = atomicAdd(&ctrl->ticket, 1u) - ticket0 + gridDim.x;
+            tslot ^= 1u;
+        }
         const uint64_t cbase = readlane64(tbv, 0), cend = readlane64(tbv, 1);
         const bool skip = cend > n || cbase >= cend;  // empty, or malformed (flagged by rl_offsets_kernel)
         s_val4[tid] = vv;
@@ -2031,12 +2047,17 @@ extern "C" int flrl_rl_decode_device(const uint8_t *d_counts, const uint8_t *d_v
     const size_t rgrid = (size_t)(wide ? rd_per_cu<kRdThreadsWide>() : rd_per_cu<kRdThreads>()) * (size_t)cu_count();
     const dim3 grid((uint32_t)(L.tiles < rgrid ? L.tiles : rgrid));
     kernel_timing_begin(s);
+    // ticket order for the 512-thread decode from eight tiles per workgroup on
+    // (four: 512 MiB runs32 +2 %; long runs, 256-thread tiles: tickets +23 %)
+    const bool tickets = wide && L.tiles >= 8 * (size_t)grid.x;
     if (wide)
         hipLaunchKernelGGL(rl_decode_kernel<kRdThreadsWide>, grid, dim3(kRdThreadsWide), 0, s, d_counts, d_values,
-                           (uint64_t)runs, d_out, (uint64_t)n, tile_base, (uint64_t)L.tiles);
+                           (uint64_t)runs, d_out, (uint64_t)n, tile_base, (uint64_t)L.tiles, ctrl,
+                           (uint32_t)L.blocks, tickets);
     else
         hipLaunchKernelGGL(rl_decode_kernel<kRdThreads>, grid, dim3(kRdThreads), 0, s, d_counts, d_values,
-                           (uint64_t)runs, d_out, (uint64_t)n, tile_base, (uint64_t)L.tiles);
+                           (uint64_t)runs, d_out, (uint64_t)n, tile_base, (uint64_t)L.tiles, ctrl,
+                           (uint32_t)L.blocks, false);
     kernel_timing_end(s);
     FLRL_HIP(hipGetLastError());
     return FLRL_OK;
