@@ -1462,15 +1462,14 @@ __global__ __launch_bounds__(T, 4) void rl_decode_kernel(  // 2nd: waves per SIM
     uint64_t tile = blockIdx.x;
     if (tile >= ntiles)
         return;
-    // tickets: later tiles by ticket, taken one tile ahead (the pre-pass took
-    // tickets 0..ticket0-1), so the workgroups move through the output together
-    // instead of drifting apart grid-stride (runs32: 1 GiB -3.5 %, 4 GiB
-    // -10 %; with two tiles per workgroup, 256 MiB, +14 %: the host asks for
-    // them from eight tiles per workgroup on)
+    // tickets: tiles from the third on by ticket, taken one tile ahead (the
+    // pre-pass took tickets 0..ticket0-1), so the workgroups move through the
+    // output together instead of drifting apart grid-stride (runs32: 1 GiB
+    // -5 %, 4 GiB -10 %, runs of 1..64 -8 %); the first two tiles are
+    // grid-stride, so no workgroup waits for a ticket at the start
     __shared__ uint32_t s_tk[2];
-    if (tickets && threadIdx.x == 0)
-        s_tk[0] = atomicAdd(&ctrl->ticket, 1u) - ticket0 + gridDim.x;
-    uint32_t tslot = 1;
+    uint32_t tslot = 0;
+    bool first_round = true;  // the second tile is grid-stride too: no ticket wait at the start
     if (tid < 256) {
         static_assert(T >= 256, "one table entry per thread");
         uint64_t e = 0;
@@ -1492,10 +1491,12 @@ __global__ __launch_bounds__(T, 4) void rl_decode_kernel(  // 2nd: waves per SIM
         __syncthreads();  // the previous tile's LDS readers are done; s_tk written
         uint64_t next = tile + gridDim.x;
         if (tickets) {
-            next = s_tk[tslot ^ 1u];
-            if (threadIdx.x == 0)
-                s_tk[tslot] = atomicAdd(&ctrl->ticket, 1u) - ticket0 + gridDim.x;
+            if (!first_round)
+                next = s_tk[tslot ^ 1u];
+            if (threadIdx.x == 0)  // the tile after next, read two barriers from now
+                s_tk[tslot] = atomicAdd(&ctrl->ticket, 1u) - ticket0 + 2u * gridDim.x;
             tslot ^= 1u;
+            first_round = false;
         }
         const uint64_t cbase = readlane64(tbv, 0), cend = readlane64(tbv, 1);
         const bool skip = cend > n || cbase >= cend;  // empty, or malformed (flagged by rl_offsets_kernel)
@@ -2047,9 +2048,9 @@ extern "C" int flrl_rl_decode_device(const uint8_t *d_counts, const uint8_t *d_v
     const size_t rgrid = (size_t)(wide ? rd_per_cu<kRdThreadsWide>() : rd_per_cu<kRdThreads>()) * (size_t)cu_count();
     const dim3 grid((uint32_t)(L.tiles < rgrid ? L.tiles : rgrid));
     kernel_timing_begin(s);
-    // ticket order for the 512-thread decode from eight tiles per workgroup on
-    // (four: 512 MiB runs32 +2 %; long runs, 256-thread tiles: tickets +23 %)
-    const bool tickets = wide && L.tiles >= 8 * (size_t)grid.x;
+    // ticket order for the 512-thread decode from FLRL_RD_TICKET_MIN tiles per
+    // workgroup on (long runs, 256-thread tiles: tickets +23 %)
+    const bool tickets = wide && L.tiles >= (size_t)FLRL_RD_TICKET_MIN * grid.x;
     if (wide)
         hipLaunchKernelGGL(rl_decode_kernel<kRdThreadsWide>, grid, dim3(kRdThreadsWide), 0, s, d_counts, d_values,
                            (uint64_t)runs, d_out, (uint64_t)n, tile_base, (uint64_t)L.tiles, ctrl,
