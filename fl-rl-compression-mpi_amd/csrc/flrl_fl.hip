@@ -511,12 +511,13 @@ __global__ __launch_bounds__(kDecThreads, kDecPerCU) void fl_decode_kernel(
     const int tid = threadIdx.x;
     const int lane = tid & (kWave - 1);
     const int wave = tid / kWave;
-    // the first tile is the workgroup's own index (no atomic round trip at the
-    // launch, when every workgroup would queue on the counter at once: -3.4 us
-    // per call); later tiles by ticket, numbered past the grid
+    // the first two tiles are grid-stride (no atomic round trip at the launch,
+    // when every workgroup would queue on the counter at once: -3.4 us, and
+    // -1 % more for the second); later tiles by ticket, numbered past them
     // (fl_offsets_kernel's workgroups took tickets 0..ticket0-1 of the same
     // counter): workgroups progress through the output in order
-    ticket0 -= gridDim.x;
+    ticket0 -= 2u * gridDim.x;
+    bool first_round = true;  // the second tile is grid-stride too (-1 %: no burst of tickets at the start)
     uint32_t tile = blockIdx.x;
     uint32_t slot = 1;
     if (tile >= ntiles)
@@ -533,7 +534,8 @@ __global__ __launch_bounds__(kDecThreads, kDecPerCU) void fl_decode_kernel(
     uint64_t wv = dec_load_widths(bits, (uint64_t)tile * TF + (tid >> 3) * ITEMS, nframes);
     for (;;) {
         if (tid == 0)  // read after the scan barrier below
-            s_next[slot] = atomicAdd(&ctrl->ticket, 1u) - ticket0;
+            s_next[slot] = first_round ? tile + gridDim.x : atomicAdd(&ctrl->ticket, 1u) - ticket0;
+        first_round = false;
 #pragma unroll
         for (int k = 0; k < ITEMS; ++k)
             if ((uint32_t)(k * T + tid) < agg)
