@@ -11,6 +11,10 @@
 // output's target is replaced, not the link. An existing output that is not a
 // regular file (/dev/null, a FIFO) is written directly, and so is one whose
 // directory does not allow a temporary (unless it is the input being read).
+// EXCEPTION to "untouched": that in-place case truncates the existing output
+// at open (as the reference's fopen(path, "wb") does), so a later failure
+// leaves it truncated or partial. Callers therefore acquire every other
+// resource that can fail up front (e.g. the RL side file) before open().
 // Header-only (POSIX), shared by libflrl.so and the CLI.
 #pragma once
 
@@ -138,13 +142,10 @@ private:
     bool direct_ = false, in_place_ = false, done_ = false;
 };
 
-// An anonymous scratch file in the directory of `near_path` (unlinked at once,
-// so it never collides with or clobbers a user file). -1 on failure.
-inline int anon_file_near(const char *near_path)
+// An anonymous scratch file in directory `dir` (unlinked at once, so it never
+// collides with or clobbers a user file). -1 on failure.
+inline int anon_file_in(const std::string &dir)
 {
-    std::string p(near_path);
-    const size_t slash = p.rfind('/');
-    const std::string dir = slash == std::string::npos ? "." : (slash == 0 ? "/" : p.substr(0, slash));
 #ifdef O_TMPFILE
     const int t = ::open(dir.c_str(), O_TMPFILE | O_RDWR, 0600);
     if (t >= 0)
@@ -157,6 +158,23 @@ inline int anon_file_near(const char *near_path)
     if (fd >= 0)
         ::unlink(buf.data());
     return fd;
+}
+
+// An anonymous scratch file next to `near_path` (same file system as the
+// output), else in $TMPDIR or /tmp when that directory allows none (the
+// read-only-directory case in which OutFile writes in place). -1 on failure.
+inline int anon_file_near(const char *near_path)
+{
+    std::string p(near_path);
+    const size_t slash = p.rfind('/');
+    const std::string dir = slash == std::string::npos ? "." : (slash == 0 ? "/" : p.substr(0, slash));
+    int fd = anon_file_in(dir);
+    if (fd >= 0)
+        return fd;
+    const char *td = ::getenv("TMPDIR");
+    if (td && *td && (fd = anon_file_in(td)) >= 0)
+        return fd;
+    return anon_file_in("/tmp");
 }
 
 }  // namespace flrl

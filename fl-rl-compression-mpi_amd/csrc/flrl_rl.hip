@@ -247,10 +247,10 @@ __device__ __forceinline__ uint64_t lookback_seg(uint64_t *status, uint32_t tile
                 return sm_const(0, 0);
             }
             const uint64_t now = __builtin_amdgcn_s_memrealtime();
-            if (!helping) {
+            if (!helping) {  // the clock starts at the first unpublished poll (help_ticks 0: help at once)
                 if (t0 == 0)
                     t0 = now;
-                else if (now - t0 >= help_ticks)
+                if (now - t0 >= help_ticks)
                     helping = true;
             }
             if (helping) {  // the oldest unpublished slot the window needs (uniform)
@@ -673,8 +673,7 @@ struct RlWave {
     // PhaseMap and natural heads; the runs of the state-independent heads are
     // staged in LDS (stc/stv) at their chunk-local index until the staging area
     // is full (nst: the sub-chunks staged completely).
-    template <class Hook>
-    __device__ void scan_chunk(uint64_t off, uint32_t len, Chunk &C, Hook &&hook) const
+    __device__ void scan_chunk(uint64_t off, uint32_t len, Chunk &C) const
     {
         C.off = off;
         C.len = len;
@@ -727,7 +726,6 @@ struct RlWave {
             rel_in = pm_compose(rel_in, L.smap);
             if (nst == SUB && indep)
                 lane_runs(L, h0, h1, cr, slot);
-            hook(s);
         }
         if (nst >= C.ns) {
             nst = C.ns;
@@ -740,36 +738,6 @@ struct RlWave {
         C.Kst = Kst;
         C.rel_in = rel_in;
         C.rel_st = rel_st;
-    }
-
-    // Staged records to / from a global slot (16-byte vectors; this wave's own).
-    __device__ void staging_to(uint8_t *gc, uint8_t *gv, uint32_t K) const
-    {
-        for (uint32_t j = (uint32_t)lane * 16; j < K; j += kWave * 16) {
-            *reinterpret_cast<u32x4 *>(gc + j) = *reinterpret_cast<const u32x4 *>(stc + j);
-            *reinterpret_cast<u32x4 *>(gv + j) = *reinterpret_cast<const u32x4 *>(stv + j);
-        }
-    }
-    __device__ void staging_from(const uint8_t *gc, const uint8_t *gv, uint32_t K) const
-    {
-        constexpr int R = (SW + kWave * 16 - 1) / (kWave * 16);
-        u32x4 a[R], b[R];
-#pragma unroll
-        for (int r = 0; r < R; ++r) {  // all loads in flight, then the LDS writes
-            const uint32_t j = (uint32_t)(r * kWave + lane) * 16;
-            if (j < K) {
-                a[r] = *reinterpret_cast<const u32x4 *>(gc + j);
-                b[r] = *reinterpret_cast<const u32x4 *>(gv + j);
-            }
-        }
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            const uint32_t j = (uint32_t)(r * kWave + lane) * 16;
-            if (j < K) {
-                *reinterpret_cast<u32x4 *>(stc + j) = a[r];
-                *reinterpret_cast<u32x4 *>(stv + j) = b[r];
-            }
-        }
     }
 
     // Sub-chunks [s0, ns) of the chunk at `off`, re-read and emitted with the
@@ -992,7 +960,7 @@ __global__ __launch_bounds__(T, kRlWavesPerSimd) void rl_encode_wave_kernel(  //
     {
         const uint64_t off = (uint64_t)tile * Wv::TBT + (uint64_t)w * Wv::CB;
         const uint32_t len = off >= n ? 0u : (n - off < (uint64_t)Wv::CB ? (uint32_t)(n - off) : (uint32_t)Wv::CB);
-        V.scan_chunk(off, len, C, [](int) {});
+        V.scan_chunk(off, len, C);
     }
     // ---- the wave maps -> the tile's map -> ONE look-back -> each wave's state
     if (V.lane == 0)
@@ -1025,196 +993,6 @@ __global__ __launch_bounds__(T, kRlWavesPerSimd) void rl_encode_wave_kernel(  //
     // it (its status words were stale too, so the output is not trusted)
     if (tid == 0 && atomicAdd(&ctrl->ticket, 1u) >= ntiles)
         raise_error(ctrl, FLRL_E_ARG);
-}
-
-// ---- RL encode in three passes (no look-back wait) ---------------------------
-// The single-pass kernel above spends a third of each tile's life waiting in
-// its look-back for the slowest predecessor's scan (trace: DESIGN §9). Here
-// (1) rl_encode_scan_kernel scans every tile independently (grid = tiles, no
-// ticket, no look-back): each wave's chunk summary and the staged runs go to
-// the scratch, the tile's composite map to tmap[tile]; (2) rl_encode_state_kernel
-// scans the tile maps (256 per workgroup, one decoupled look-back per
-// workgroup) into each tile's incoming state (heads before it, chunk state);
-// (3) rl_encode_emit_kernel gives every wave its state (the tile's, advanced by
-// the maps of the waves before it), brings its staged runs back into LDS and
-// emits exactly as the single-pass kernel (split heads, staged runs, re-read
-// sub-chunks past a staging overflow, the final run). Extra traffic: the staged
-// runs out and back (4 bytes per staged run).
-template <int LB, int SUB, int W>
-struct RlChunkSum {  // a wave's Chunk in 48 bytes
-    using Wv = RlWave<LB, SUB, W>;
-    __device__ static void put(u32x4 *dst, const typename Wv::Chunk &C)
-    {
-        dst[0] = u32x4{(uint32_t)C.off, (uint32_t)(C.off >> 32), C.len, (uint32_t)C.ns};
-        dst[1] = u32x4{(uint32_t)C.nst, C.first, C.K, C.Kst};
-        dst[2] = u32x4{C.rel_in, C.rel_st, C.v0, 0u};
-    }
-    __device__ static typename Wv::Chunk get(const u32x4 *src)
-    {
-        typename Wv::Chunk C;
-        const u32x4 a = src[0], b = src[1], c = src[2];
-        C.off = ((uint64_t)a[1] << 32) | a[0];
-        C.len = a[2];
-        C.ns = (int)a[3];
-        C.nst = (int)b[0];
-        C.first = b[1];
-        C.K = b[2];
-        C.Kst = b[3];
-        C.rel_in = c[0];
-        C.rel_st = c[1];
-        C.v0 = c[2];
-        return C;
-    }
-};
-
-template <int T, int LB, int SUB>
-__global__ __launch_bounds__(T, kRlWavesPerSimd) void rl_encode_scan_kernel(const uint8_t *__restrict__ in, uint64_t n,
-                                                           uint64_t *__restrict__ tmap, u32x4 *__restrict__ sums,
-                                                           uint8_t *__restrict__ gstage)
-{
-    constexpr int W = T / kWave;
-    using Wv = RlWave<LB, SUB, W>;
-    __shared__ __attribute__((aligned(16))) uint8_t s_lds[Wv::kLdsBytes];
-    __shared__ uint64_t s_map[W];
-    const int w = threadIdx.x / kWave;
-    const Wv V(in, n, s_lds, w);
-    const uint32_t tile = blockIdx.x;
-    typename Wv::Chunk C;
-    const uint64_t off = (uint64_t)tile * Wv::TBT + (uint64_t)w * Wv::CB;
-    const uint32_t len = off >= n ? 0u : (n - off < (uint64_t)Wv::CB ? (uint32_t)(n - off) : (uint32_t)Wv::CB);
-    V.scan_chunk(off, len, C, [](int) {});
-    uint8_t *gs = gstage + (uint64_t)tile * kRlStageBytes + (uint64_t)w * 2 * Wv::SW;
-    wave_lds_sync();  // the staging writes of all lanes first
-    V.staging_to(gs, gs + Wv::SW, C.Kst);
-    if (V.lane == 0) {
-        RlChunkSum<LB, SUB, W>::put(sums + ((uint64_t)tile * W + w) * 3, C);
-        s_map[w] = C.map();
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        uint64_t m = s_map[0];
-#pragma unroll
-        for (int v = 1; v < W; ++v)
-            m = sm_compose(m, s_map[v]);
-        tmap[tile] = m;
-    }
-}
-
-// inclusive wave scan of segment maps (oldest first; lanes without a source
-// read 0 = the identity map "no natural head, 0 bytes")
-
-constexpr int kRsThreads = 256;  // tile maps per state-scan workgroup
-
-// Tile states by reduce-then-scan in one launch: every workgroup scans its 256
-// tile maps (packed: <= 32 MiB of input, within the 26-bit fields) into
-// in-block exclusive prefixes (tlocal) and stores its aggregate unpacked
-// (kind, L or pre, K, c); the last workgroup to finish (a counter) applies the
-// aggregates in order to the state (H, c), from (0, 0), and writes each
-// block's incoming state (bpre: H, c). A tile's state is then
-// sm_compose(bpre[tile / 256] as Const, tlocal[tile]) (rl_encode_emit_kernel).
-__global__ __launch_bounds__(kRsThreads) void rl_encode_state_kernel(const uint64_t *__restrict__ tmap,
-                                                                     uint32_t ntiles, uint32_t nblocks,
-                                                                     uint64_t *__restrict__ tlocal,
-                                                                     uint64_t *__restrict__ bagg,
-                                                                     uint64_t *__restrict__ bpre, Ctrl *ctrl)
-{
-    constexpr int NW = kRsThreads / kWave;
-    __shared__ uint64_t s_w[NW];
-    __shared__ uint32_t s_last;
-    const int tid = threadIdx.x;
-    const int lane = tid & (kWave - 1);
-    const int wave = tid / kWave;
-    const uint32_t blk = blockIdx.x;
-    const uint32_t t = blk * kRsThreads + tid;
-    const uint64_t m = t < ntiles ? tmap[t] : sm_nonat(0);
-    const uint64_t inc = wave_incl_scan_sm(m);
-    if (lane == kWave - 1)
-        s_w[wave] = inc;
-    __syncthreads();
-    uint64_t before = sm_nonat(0), agg = sm_nonat(0);  // waves before this one; the whole block
-#pragma unroll
-    for (int v = 0; v < NW; ++v) {
-        const uint64_t x = s_w[v];
-        if (v < wave)
-            before = sm_compose(before, x);
-        agg = sm_compose(agg, x);
-    }
-    if (t < ntiles)
-        tlocal[t] = sm_compose(before, wave_shr1_64(inc));  // lane 0 reads the identity
-    if (tid == 0) {
-        const bool nat = (agg & kSmKind) == kSmNat;
-        bagg[4 * blk + 0] = nat ? 1 : 0;
-        bagg[4 * blk + 1] = sm_a(agg);
-        bagg[4 * blk + 2] = nat ? sm_b(agg) : 0;
-        bagg[4 * blk + 3] = sm_c(agg);
-        __threadfence();  // the aggregate before the count
-        const uint32_t k = atomicAdd(&ctrl->ticket, 1u);
-        if (k >= nblocks)  // the scratch's counter was not reset for this launch
-            raise_error(ctrl, FLRL_E_ARG);
-        s_last = k == nblocks - 1;
-    }
-    __syncthreads();
-    if (!s_last)
-        return;
-    // the last block: every aggregate into LDS (all loads in flight at once, past
-    // the L1), then thread 0 applies them in order
-    __threadfence();  // every block's aggregate is visible
-    __shared__ uint64_t s_agg[kRsThreads][4];
-    uint64_t H = 0;
-    uint32_t c = 0;
-    for (uint32_t b0 = 0; b0 < nblocks; b0 += kRsThreads) {
-        const uint32_t b = b0 + tid;
-        if (b < nblocks) {
-#pragma unroll
-            for (int f = 0; f < 4; ++f)
-                s_agg[tid][f] = granule_load(&bagg[4 * b + f]);
-        }
-        __syncthreads();
-        if (tid == 0) {
-            const uint32_t nb = nblocks - b0 < (uint32_t)kRsThreads ? nblocks - b0 : (uint32_t)kRsThreads;
-            for (uint32_t i = 0; i < nb; ++i) {
-                bpre[2 * (b0 + i)] = H;
-                bpre[2 * (b0 + i) + 1] = c;
-                const uint64_t a = s_agg[i][1];
-                if (s_agg[i][0]) {
-                    H += splits64(c, a) + s_agg[i][2];
-                    c = (uint32_t)s_agg[i][3];
-                } else {
-                    H += splits64(c, a);
-                    c = add_c64(c, a);
-                }
-            }
-        }
-        __syncthreads();
-    }
-}
-
-template <int T, int LB, int SUB>
-__global__ __launch_bounds__(T, kRlWavesPerSimd) void rl_encode_emit_kernel(const uint8_t *__restrict__ in, uint64_t n,
-                                                           const u32x4 *__restrict__ sums,
-                                                           const uint64_t *__restrict__ tlocal,
-                                                           const uint64_t *__restrict__ bpre,
-                                                           const uint8_t *__restrict__ gstage,
-                                                           uint8_t *__restrict__ counts, uint8_t *__restrict__ values,
-                                                           uint64_t *__restrict__ runs_out)
-{
-    constexpr int W = T / kWave;
-    using Wv = RlWave<LB, SUB, W>;
-    using Sum = RlChunkSum<LB, SUB, W>;
-    __shared__ __attribute__((aligned(16))) uint8_t s_lds[Wv::kLdsBytes];
-    const int w = threadIdx.x / kWave;
-    const Wv V(in, n, s_lds, w);
-    const uint32_t tile = blockIdx.x;
-    const u32x4 *ts = sums + (uint64_t)tile * W * 3;
-    const uint32_t sb = tile / kRsThreads;
-    uint64_t st = sm_compose(sm_const(bpre[2 * sb], (uint32_t)bpre[2 * sb + 1]), tlocal[tile]);
-    for (int v = 0; v < w; ++v)
-        st = sm_compose(st, Sum::get(ts + 3 * v).map());
-    const typename Wv::Chunk C = Sum::get(ts + 3 * w);
-    const uint8_t *gs = gstage + (uint64_t)tile * kRlStageBytes + (uint64_t)w * 2 * Wv::SW;
-    V.staging_from(gs, gs + Wv::SW, C.Kst);
-    wave_lds_sync();
-    V.emit(C, sm_h(st), sm_c(st), counts, values, runs_out);
 }
 
 // ---- decode pre-pass: output offsets of each decode tile ------------------
@@ -1848,31 +1626,14 @@ __global__ __launch_bounds__(kWdThreads) void rl_decode_wave_kernel(
     }
 }
 
-// single pass: [Ctrl][status: tiles] (zeroed); three passes: [Ctrl] (zeroed)
-// [tmap: tiles][tlocal: tiles][bagg: blocks x 32 B][bpre: blocks x 16 B]
-// [sums: tiles x 4 x 48 B][staged runs: tiles x kRlStageBytes]
+// [Ctrl][status: tiles, one 128-B line each] (zeroed per call)
 struct RlEncLayout {
-    size_t tiles, sblocks, zero, o_status, o_tmap, o_tstate, o_bagg, o_bpre, o_sums, o_stage, bytes;
-    explicit RlEncLayout(size_t n, bool three)
+    size_t tiles, zero, bytes;
+    explicit RlEncLayout(size_t n)
     {
         tiles = div_up(n, (size_t)kRlTileBytes);
-        if (!three) {
-            sblocks = 0;
-            o_status = kRlStatusOff;
-            zero = kRlStatusOff + round_up(tiles * 8 * kRlStatusStride, 16);  // ticket, error, status
-            o_tmap = o_tstate = o_bagg = o_bpre = o_sums = o_stage = bytes = zero;
-            return;
-        }
-        sblocks = div_up(tiles, (size_t)kRsThreads);
-        zero = sizeof(Ctrl);  // the state kernel's block counter
-        o_status = zero;
-        o_tmap = zero;
-        o_tstate = o_tmap + round_up(tiles * 8, 16);   // tlocal
-        o_bagg = o_tstate + round_up(tiles * 8, 16);
-        o_bpre = o_bagg + sblocks * 32;
-        o_sums = o_bpre + sblocks * 16;
-        o_stage = o_sums + tiles * (kRlThreads / kWave) * 48;
-        bytes = o_stage + tiles * (size_t)kRlStageBytes;
+        zero = kRlStatusOff + round_up(tiles * 8 * kRlStatusStride, 16);  // ticket, error, status
+        bytes = zero;
     }
 };
 
@@ -1901,32 +1662,15 @@ struct RlDecLayout {
 
 using namespace flrl;
 
-static bool rl_form_known(int form) { return form == FLRL_RL_FORM_LOOKBACK || form == FLRL_RL_FORM_THREE_PASS; }
-
-extern "C" size_t flrl_rl_scratch_bytes_form(size_t n, int form)
-{
-    return rl_form_known(form) ? RlEncLayout(n, form == FLRL_RL_FORM_THREE_PASS).bytes : 0;
-}
-extern "C" size_t flrl_rl_scratch_bytes(size_t n) { return flrl_rl_scratch_bytes_form(n, FLRL_RL_FORM_LOOKBACK); }
+extern "C" size_t flrl_rl_scratch_bytes(size_t n) { return RlEncLayout(n).bytes; }
 extern "C" size_t flrl_rl_decode_scratch_bytes(size_t runs) { return RlDecLayout(runs).bytes; }
 
 extern "C" int flrl_rl_encode_device(const uint8_t *d_in, size_t n, uint8_t *d_counts,
                                      uint8_t *d_values, uint64_t *d_runs, void *d_scratch,
                                      size_t scratch_bytes, void *stream)
 {
-    return flrl_rl_encode_device_form(d_in, n, d_counts, d_values, d_runs, d_scratch, scratch_bytes, stream,
-                                      FLRL_RL_FORM_LOOKBACK);
-}
-
-extern "C" int flrl_rl_encode_device_form(const uint8_t *d_in, size_t n, uint8_t *d_counts,
-                                          uint8_t *d_values, uint64_t *d_runs, void *d_scratch,
-                                          size_t scratch_bytes, void *stream, int form)
-{
     hipStream_t s = static_cast<hipStream_t>(stream);
-    if (!rl_form_known(form))
-        return set_error(FLRL_E_ARG, "flrl_rl_encode_device_form: unknown form %d", form);
-    const bool three = form == FLRL_RL_FORM_THREE_PASS;
-    const RlEncLayout L(n, three);
+    const RlEncLayout L(n);
     if (!d_runs || !d_scratch)
         return set_error(FLRL_E_ARG, "flrl_rl_encode_device: null runs/scratch");
     if (scratch_bytes < L.bytes)
@@ -1934,12 +1678,8 @@ extern "C" int flrl_rl_encode_device_form(const uint8_t *d_in, size_t n, uint8_t
                          scratch_bytes, L.bytes);
     if (!aligned16(d_scratch))
         return set_error(FLRL_E_ARG, "flrl_rl_encode_device: scratch not 16-byte aligned");
-    if (three) {
-        FLRL_HIP(scratch_reset(d_scratch, L.zero, s));
-    } else {
-        static_assert(kRlStatusOff % 16 == 0 && kRlStatusOff >= sizeof(Ctrl), "Ctrl area");
-        FLRL_HIP(scratch_reset_strided(d_scratch, kRlStatusOff, L.tiles, 8 * kRlStatusStride, s));
-    }
+    static_assert(kRlStatusOff % 16 == 0 && kRlStatusOff >= sizeof(Ctrl), "Ctrl area");
+    FLRL_HIP(scratch_reset_strided(d_scratch, kRlStatusOff, L.tiles, 8 * kRlStatusStride, s));
     if (n == 0) {
         FLRL_HIP(zero_async(d_runs, sizeof(uint64_t), s));
         return FLRL_OK;
@@ -1951,28 +1691,11 @@ extern "C" int flrl_rl_encode_device_form(const uint8_t *d_in, size_t n, uint8_t
     if (L.tiles > 0xFFFFFFFFull)
         return set_error(FLRL_E_ARG, "flrl_rl_encode_device: input too large");
     Ctrl *ctrl = static_cast<Ctrl *>(d_scratch);
-    uint8_t *base = static_cast<uint8_t *>(d_scratch);
-    kernel_timing_begin(s);  // the hook brackets every pass of the encode
-    if (three) {
-        uint64_t *tmap = reinterpret_cast<uint64_t *>(base + L.o_tmap);
-        uint64_t *tlocal = reinterpret_cast<uint64_t *>(base + L.o_tstate);
-        uint64_t *bagg = reinterpret_cast<uint64_t *>(base + L.o_bagg);
-        uint64_t *bpre = reinterpret_cast<uint64_t *>(base + L.o_bpre);
-        u32x4 *sums = reinterpret_cast<u32x4 *>(base + L.o_sums);
-        uint8_t *stage = base + L.o_stage;
-        hipLaunchKernelGGL((rl_encode_scan_kernel<kRlThreads, kRlLaneBytes, kRlSub>), dim3((uint32_t)L.tiles),
-                           dim3(kRlThreads), 0, s, d_in, (uint64_t)n, tmap, sums, stage);
-        hipLaunchKernelGGL(rl_encode_state_kernel, dim3((uint32_t)L.sblocks), dim3(kRsThreads), 0, s, tmap,
-                           (uint32_t)L.tiles, (uint32_t)L.sblocks, tlocal, bagg, bpre, ctrl);
-        hipLaunchKernelGGL((rl_encode_emit_kernel<kRlThreads, kRlLaneBytes, kRlSub>), dim3((uint32_t)L.tiles),
-                           dim3(kRlThreads), 0, s, d_in, (uint64_t)n, sums, tlocal, bpre, stage, d_counts,
-                           d_values, d_runs);
-    } else {
-        uint64_t *status = reinterpret_cast<uint64_t *>(base + L.o_status);
-        hipLaunchKernelGGL((rl_encode_wave_kernel<kRlThreads, kRlLaneBytes, kRlSub>), dim3((uint32_t)L.tiles),
-                           dim3(kRlThreads), 0, s, d_in, (uint64_t)n, (uint32_t)L.tiles, d_counts, d_values,
-                           d_runs, ctrl, status, lookback_help_ticks(kRlHelpTicks));
-    }
+    uint64_t *status = reinterpret_cast<uint64_t *>(static_cast<uint8_t *>(d_scratch) + kRlStatusOff);
+    kernel_timing_begin(s);
+    hipLaunchKernelGGL((rl_encode_wave_kernel<kRlThreads, kRlLaneBytes, kRlSub>), dim3((uint32_t)L.tiles),
+                       dim3(kRlThreads), 0, s, d_in, (uint64_t)n, (uint32_t)L.tiles, d_counts, d_values,
+                       d_runs, ctrl, status, lookback_help_ticks(kRlHelpTicks));
     kernel_timing_end(s);
     FLRL_HIP(hipGetLastError());
     return FLRL_OK;

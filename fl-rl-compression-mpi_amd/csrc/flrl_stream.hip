@@ -317,8 +317,11 @@ struct MemFl {  // FL arrays in host memory
 // last; past kPoolBytes of idle pinned memory the least recently used sets are
 // freed (a set holds as much HBM as pinned memory), and flrl_release_staging
 // frees every idle set. The host-buffer API's 8 pipelines of 16 MiB chunks
-// hold 512 MiB of pinned memory per direction (compress, decompress).
-constexpr size_t kPoolBytes = 1ull << 30;
+// hold 8 x 2 x (16 MiB + 128 KiB + 16 MiB + 16) ~ 514 MiB of pinned memory per
+// direction (compress, decompress); the cap keeps both directions' sets (plus
+// slack), so alternating compress and decompress never reallocates.
+constexpr size_t kHostSetBound = 2 * (2 * (size_t)FLRL_HOST_CHUNK + (size_t)FLRL_HOST_CHUNK / 128 + 16);
+constexpr size_t kPoolBytes = 2 * (size_t)FLRL_HOST_WORKERS * kHostSetBound + (64ull << 20);
 struct PoolKey {
     int dev;
     size_t a, b, c, scr;
@@ -1020,11 +1023,14 @@ extern "C" int flrl_rl_compress_file(const char *in_path, const char *out_path, 
     if (::fstat(in.fd, &st) != 0)
         return set_error(FLRL_E_ARG, "[FileIO] Cannot stat file: %s", in_path);
     const uint64_t n = (uint64_t)st.st_size;
+    // values[] until R is known: an anonymous file next to the output (else in
+    // $TMPDIR or /tmp). Created BEFORE the output is opened: an output in a
+    // read-only directory is truncated in place at open (OutFile), so nothing
+    // that can fail may come between that open and the first write
+    if ((side.fd = anon_file_near(out_path)) < 0)
+        return set_error(FLRL_E_ARG, "[FileIO] Cannot create a temporary file for %s", out_path);
     if (!out.open(out_path, false, in.fd))
         return set_error(FLRL_E_ARG, "[FileIO] Cannot open file: %s", out_path);
-    // values[] until R is known: an anonymous file next to the output
-    if ((side.fd = anon_file_near(out_path)) < 0)
-        return set_error(FLRL_E_ARG, "[FileIO] Cannot create a temporary file next to %s", out_path);
     const size_t chunk = requested_or(chunk_bytes);
     const size_t nchunks = n ? (size_t)((n + chunk - 1) / chunk) : 0;
 

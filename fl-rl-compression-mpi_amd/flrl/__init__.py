@@ -120,9 +120,7 @@ _sig("flrl_rl_compress", ctypes.c_int, _vp, _sz, ctypes.POINTER(_RLBuf))
 _sig("flrl_rl_decompress", ctypes.c_int, _sz, _vp, _vp, _sz,
      ctypes.POINTER(_u8p), ctypes.POINTER(_sz))
 _sig("flrl_rl_scratch_bytes", _sz, _sz)
-_sig("flrl_rl_scratch_bytes_form", _sz, _sz, ctypes.c_int)
 _sig("flrl_rl_encode_device", ctypes.c_int, _vp, _sz, _vp, _vp, _vp, _vp, _sz, _vp)
-_sig("flrl_rl_encode_device_form", ctypes.c_int, _vp, _sz, _vp, _vp, _vp, _vp, _sz, _vp, ctypes.c_int)
 _sig("flrl_rl_decode_scratch_bytes", _sz, _sz)
 _sig("flrl_rl_decode_device", ctypes.c_int, _vp, _vp, _sz, _vp, _sz, _vp, _sz, _vp)
 _sig("flrl_gen_device", ctypes.c_int, ctypes.c_int, _u64, _u64, _vp, _sz, _vp)
@@ -146,8 +144,6 @@ _sig("flrl_fl_encode_sharded", ctypes.c_int, _vp, ctypes.c_int, _pp, ctypes.POIN
      _pp, _pp, ctypes.POINTER(_sz), _pp)
 
 UNIQUE_ID_BYTES = 128
-# RL encode forms (include/flrl.h FLRL_RL_FORM_*)
-RL_FORM_LOOKBACK, RL_FORM_THREE_PASS = 1, 3
 # per-shard sizes record written by the exchange (include/flrl.h FLRL_SZ_*)
 SZ_F, SZ_V, SZ_F_OFF, SZ_V_OFF, SZ_F_TOTAL, SZ_V_TOTAL, SZ_COUNT = range(7)
 
@@ -409,8 +405,8 @@ def fl_values_capacity(n: int) -> int:
     return int(_lib.flrl_fl_values_capacity(n))
 
 
-def rl_scratch_bytes(n: int, form: int = RL_FORM_LOOKBACK) -> int:
-    return int(_lib.flrl_rl_scratch_bytes_form(n, form))
+def rl_scratch_bytes(n: int) -> int:
+    return int(_lib.flrl_rl_scratch_bytes(n))
 
 
 def rl_decode_scratch_bytes(runs: int) -> int:
@@ -430,10 +426,9 @@ def fl_decode_device(d_bits: int, bits_size: int, d_values: int, values_size: in
 
 
 def rl_encode_device(d_in: int, n: int, d_counts: int, d_values: int, d_runs: int,
-                     d_scratch: int, scratch_bytes: int, stream: int = 0,
-                     form: int = RL_FORM_LOOKBACK) -> None:
-    _check(_lib.flrl_rl_encode_device_form(d_in, n, d_counts, d_values, d_runs, d_scratch,
-                                           scratch_bytes, stream or None, form))
+                     d_scratch: int, scratch_bytes: int, stream: int = 0) -> None:
+    _check(_lib.flrl_rl_encode_device(d_in, n, d_counts, d_values, d_runs, d_scratch,
+                                      scratch_bytes, stream or None))
 
 
 def rl_decode_device(d_counts: int, d_values: int, runs: int, d_out: int, n: int,

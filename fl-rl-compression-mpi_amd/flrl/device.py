@@ -88,17 +88,15 @@ class FLDevice:
 
 
 class RLDevice:
-    """RL encode/decode of an n-byte buffer (build-defined format); `form` is
-    the encode form (flrl.RL_FORM_LOOKBACK or flrl.RL_FORM_THREE_PASS)."""
+    """RL encode/decode of an n-byte buffer (build-defined format)."""
 
-    def __init__(self, n: int, device: str | torch.device = "cuda", form: int = flrl.RL_FORM_LOOKBACK):
+    def __init__(self, n: int, device: str | torch.device = "cuda"):
         self.n = n
-        self.form = form
         dev = torch.device(device)
         self.counts = torch.empty(_round16(n), dtype=torch.uint8, device=dev)
         self.values = torch.empty(_round16(n), dtype=torch.uint8, device=dev)
         self.runs_t = torch.zeros(2, dtype=torch.int64, device=dev)
-        self.scratch_bytes = max(flrl.rl_scratch_bytes(n, form), flrl.rl_decode_scratch_bytes(n))
+        self.scratch_bytes = max(flrl.rl_scratch_bytes(n), flrl.rl_decode_scratch_bytes(n))
         self.scratch = torch.empty(_round16(self.scratch_bytes), dtype=torch.uint8, device=dev)
         self.out = torch.empty(_round16(n), dtype=torch.uint8, device=dev)
 
@@ -106,7 +104,7 @@ class RLDevice:
         _check_input(x, self.n)
         flrl.rl_encode_device(x.data_ptr(), self.n, self.counts.data_ptr(), self.values.data_ptr(),
                               self.runs_t.data_ptr(), self.scratch.data_ptr(), self.scratch_bytes,
-                              _stream_handle(stream), self.form)
+                              _stream_handle(stream))
 
     def decode(self, runs: int, counts: torch.Tensor | None = None,
                values: torch.Tensor | None = None, out: torch.Tensor | None = None,

@@ -76,8 +76,9 @@ int flrl_fl_compress(const uint8_t *data, size_t size, flrl_fl_buf *out);
 
 /* The host-buffer and file paths keep their pinned staging and device buffers
  * for later calls (per device and chunk shape; after a flrl_fl_compress plus a
- * flrl_fl_decompress: 1 GiB of pinned host memory and 1 GiB of HBM). Idle sets
- * are capped at 1 GiB of pinned memory (least recently used freed first) and
+ * flrl_fl_decompress: ~1 GiB of pinned host memory and ~1 GiB of HBM). Idle
+ * sets are capped at both directions' sets plus 64 MiB (~1.07 GiB of pinned
+ * memory; least recently used freed first) and
  * freed when an allocation fails; this frees every idle set now and returns
  * the pinned bytes released (sets in use by running calls are not touched). */
 size_t flrl_release_staging(void);
@@ -277,25 +278,12 @@ int flrl_rl_decompress(size_t output_size, const uint8_t *counts, const uint8_t 
 
 /* ---- RL, device-resident (asynchronous) ----------------------------------
  * d_counts / d_values capacity n bytes each; d_runs receives R (device u64).
- * Two encode forms give the same output:
- *   FLRL_RL_FORM_LOOKBACK   one kernel; tiles chained by a decoupled look-back
- *                           (the default: flrl_rl_encode_device / _scratch_bytes)
- *   FLRL_RL_FORM_THREE_PASS scan / state / emit kernels with no look-back wait;
- *                           a larger scratch (about 12 % of n). Faster when the
- *                           encode follows reads, equal after a large write
- *                           (DESIGN.md §4 "RL encode").
- * The form is an explicit argument, so sizing is a pure function of (n, form):
- * size the scratch with the form you launch. An unknown form sizes to 0 and
- * fails with FLRL_E_ARG. */
-#define FLRL_RL_FORM_LOOKBACK 1
-#define FLRL_RL_FORM_THREE_PASS 3
+ * One kernel: 128 KiB tiles chained by a decoupled look-back (DESIGN.md §4
+ * "RL encode"). (A three-pass scan / state / emit form without the look-back
+ * wait was removed in round 4: it lost alone and in the encode/decode loop.) */
 size_t flrl_rl_scratch_bytes(size_t n);
-size_t flrl_rl_scratch_bytes_form(size_t n, int form);
 int flrl_rl_encode_device(const uint8_t *d_in, size_t n, uint8_t *d_counts, uint8_t *d_values,
                           uint64_t *d_runs, void *d_scratch, size_t scratch_bytes, void *stream);
-int flrl_rl_encode_device_form(const uint8_t *d_in, size_t n, uint8_t *d_counts, uint8_t *d_values,
-                               uint64_t *d_runs, void *d_scratch, size_t scratch_bytes, void *stream,
-                               int form);
 /* Decode R runs into n = sum(counts) bytes; flags FLRL_E_FORMAT in scratch if a
  * count is 0 or the counts do not sum to n. */
 size_t flrl_rl_decode_scratch_bytes(size_t runs);

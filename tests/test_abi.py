@@ -102,34 +102,23 @@ def test_scratch_sizes_monotone():
         assert sizes == sorted(sizes), f.__name__
 
 
-@pytest.mark.parametrize("form", [flrl.RL_FORM_LOOKBACK, flrl.RL_FORM_THREE_PASS])
-def test_rl_encode_scratch_per_form(form):
-    # the encode form is an explicit argument of the sizing (a pure function of
-    # (n, form)): the three-pass form stages runs in the scratch (about 12 % of
-    # n), the single pass needs only its tile states; both grow with n
+def test_rl_encode_scratch_small():
+    # the single-pass encode needs only its tile states (one 128-byte status
+    # line per 128 KiB tile): under 1 % of n, growing with n
     pts = [1, 4096, 131072, 131073, 10 ** 6, 1 << 30]
-    sizes = [flrl.rl_scratch_bytes(x, form) for x in pts]
+    sizes = [flrl.rl_scratch_bytes(x) for x in pts]
     assert sizes == sorted(sizes)
-    big = flrl.rl_scratch_bytes(1 << 30, form)
-    if form == flrl.RL_FORM_THREE_PASS:
-        assert (1 << 30) // 10 < big < (1 << 30) // 5
-    else:
-        assert big < (1 << 30) // 100
-        assert big == flrl.rl_scratch_bytes(1 << 30) == flrl.lib_handle().flrl_rl_scratch_bytes(1 << 30)
+    big = flrl.rl_scratch_bytes(1 << 30)
+    assert big < (1 << 30) // 100
+    assert big == flrl.lib_handle().flrl_rl_scratch_bytes(1 << 30)
 
 
-def test_rl_encode_form_ignores_environment(monkeypatch):
-    # the round-2 environment switch is gone: sizing does not read it
-    before = flrl.rl_scratch_bytes(1 << 30)
-    monkeypatch.setenv("FLRL_RL_ENCODE_PASSES", "3")
-    assert flrl.rl_scratch_bytes(1 << 30) == before
-
-
-def test_rl_encode_unknown_form():
-    assert flrl.rl_scratch_bytes(1 << 20, 2) == 0
-    # rejected before any device work (no GPU needed)
-    rc = flrl.lib_handle().flrl_rl_encode_device_form(None, 0, None, None, None, None, 0, None, 2)
-    assert rc == flrl.E_ARG
+def test_three_pass_form_removed():
+    # round 4: the scan/state/emit form and its entry points are gone
+    import ctypes
+    lib = ctypes.CDLL(flrl.LIB_PATH)
+    for sym in ("flrl_rl_encode_device_form", "flrl_rl_scratch_bytes_form"):
+        assert not hasattr(lib, sym), sym
 
 
 def test_tuning_overrides_need_the_tuning_build(tmp_path):

@@ -25,43 +25,15 @@ def _need_gpu():
         pytest.fail("GPU tests need a HIP device")
 
 
-@pytest.fixture(params=[flrl.RL_FORM_LOOKBACK, flrl.RL_FORM_THREE_PASS], ids=["lookback", "3pass"])
-def passes(request):
-    """Encode tests run with both encode forms (an explicit C-ABI argument):
-    the single look-back pass (the default, reached through the host API
-    flrl_rl_compress) and the scan/state/emit passes (flrl_rl_encode_device_form)."""
-    return request.param
-
-
-FORM = flrl.RL_FORM_LOOKBACK  # the form check() encodes with; set per test by _form
-
-
-@pytest.fixture(autouse=True)
-def _form(request):
-    global FORM
-    FORM = request.getfixturevalue("passes") if "passes" in request.fixturenames else flrl.RL_FORM_LOOKBACK
-    yield
-    FORM = flrl.RL_FORM_LOOKBACK
-
-
-def encode(a: np.ndarray, form: int):
-    """RL records of `a` from the encode form under test: the host API for the
-    default form, the device API with the form argument otherwise."""
-    if form == flrl.RL_FORM_LOOKBACK:
-        r = flrl.rl_compress(a)
-        assert r.input_size == a.size
-        return r.counts, r.values
-    from flrl.device import RLDevice
-    d = RLDevice(a.size, form=form)
-    x = torch.from_numpy(np.ascontiguousarray(a)).cuda()
-    d.encode(x)
-    R = d.runs()
-    assert d.error() == 0
-    return d.counts[:R].cpu().numpy(), d.values[:R].cpu().numpy()
+def encode(a: np.ndarray):
+    """RL records of `a` through the host API (flrl_rl_compress)."""
+    r = flrl.rl_compress(a)
+    assert r.input_size == a.size
+    return r.counts, r.values
 
 
 def check(a: np.ndarray):
-    rc, rv = encode(a, FORM)
+    rc, rv = encode(a)
     counts, values = oracle.rl_compress(a)
     assert rc.size == counts.size, (rc.size, counts.size)
     assert np.array_equal(rc, counts)
@@ -71,10 +43,10 @@ def check(a: np.ndarray):
     return flrl.RLCompressed(rc, rv, a.size)
 
 
-def test_kats(golden, passes):
+def test_kats(golden):
     for case in golden["rl_kat"]:
         data = np.frombuffer(kat_input(case), np.uint8)
-        c, v = encode(data, passes)
+        c, v = encode(data)
         assert c.tolist() == case["counts"], case["name"]
         assert v.tolist() == case["values"], case["name"]
         assert flrl.rl_decompress(data.size, c, v).tobytes() == data.tobytes()
@@ -92,13 +64,13 @@ SIZES = [1, 2, 15, 16, 17, 255, 256, 257, 1023, 1024, 1025, 16383, 16384, 16385,
 
 @pytest.mark.parametrize("n", SIZES)
 @pytest.mark.parametrize("kind", ["runs32", "longruns", "u8", "zero"])
-def test_sizes_vs_oracle(n, kind, passes):
+def test_sizes_vs_oracle(n, kind):
     check(oracle.gen(kind, n, 17))
 
 
 @pytest.mark.parametrize("L", [254, 255, 256, 509, 510, 511, 16384 + 3, 131072 + 255, 400_000])
 @pytest.mark.parametrize("start", [0, 1, 15, 16, 1023, 16380, 32767, 32768, 65535, 65536, 98304, 131070])
-def test_long_run_splits(L, start, passes):
+def test_long_run_splits(L, start):
     # one long run of 7s starting at `start` inside random data
     rng = np.random.default_rng(L + start)
     a = rng.integers(0, 256, size=start + L + 300, dtype=np.uint8)
@@ -110,7 +82,7 @@ def test_long_run_splits(L, start, passes):
     check(a)
 
 
-def test_runs_spanning_many_tiles(passes):
+def test_runs_spanning_many_tiles():
     # alternating long runs of 1..3 tiles, so most tiles have no natural head
     parts = []
     rng = np.random.default_rng(3)
@@ -220,7 +192,7 @@ def test_debug_lookback_help_us_rejects_below_minus_one():
 
 
 @pytest.mark.parametrize("quiet", [1, 32768 - 3, 32768 + 100, 65536 - 3, 98304 + 7, 131072 + 5])
-def test_first_natural_head_late(quiet, passes):
+def test_first_natural_head_late(quiet):
     # no natural head for `quiet` bytes (in the first 32 KiB sub-tile, at and
     # after sub-tile boundaries, in the last sub-tile, in the next tile), then
     # mixed data
@@ -232,7 +204,7 @@ def test_first_natural_head_late(quiet, passes):
 
 
 @pytest.mark.parametrize("maxrun", [6, 12, 20, 28, 40])
-def test_medium_density(maxrun, passes):
+def test_medium_density(maxrun):
     # mean runs around the staging threshold (state-independent runs per tile
     # vs the LDS staging capacity): the staging overflows in the first, second,
     # third or last 32 KiB sub-tile of a tile, or not at all
@@ -248,7 +220,7 @@ def test_decode_offsets_rounds():
     check(oracle.gen("u8", (72 << 20) + 999, 23))
 
 
-def test_all_zero_large(passes):
+def test_all_zero_large():
     a = np.zeros(5 * 131072 + 77, np.uint8)  # no natural head after byte 0
     r = check(a)
     assert r.counts.tolist()[:3] == [255, 255, 255]
@@ -264,7 +236,7 @@ def test_decode_rejects_malformed():
         flrl.rl_decompress(3, np.zeros(0, np.uint8), np.zeros(0, np.uint8))
 
 
-def test_device_1gib_runs32(passes):
+def test_device_1gib_runs32():
     """Config #3: RL encode/decode of 1 GiB runs32 (mean run 32) — bit-exact vs
     the oracle over the full buffer and a device round trip."""
     from flrl.device import RLDevice
@@ -272,7 +244,7 @@ def test_device_1gib_runs32(passes):
     a = oracle.gen("runs32", n, 42)
     counts, values = oracle.rl_compress(a)
     x = torch.from_numpy(a).cuda()
-    d = RLDevice(n, form=passes)
+    d = RLDevice(n)
     d.encode(x)
     R = d.runs()
     assert d.error() == 0
@@ -367,7 +339,7 @@ def test_decode_wave_rejects_zero_count():
         assert e.value.code == flrl.E_FORMAT
 
 
-def test_device_more_than_2_32_runs(passes):
+def test_device_more_than_2_32_runs():
     """64-bit run indices: ~4.27 GiB of random bytes has R > 2^32 runs (all
     shorter than 255). Device round trip; R against an independent torch count
     of run starts; and the records of three windows that start at run starts
@@ -375,7 +347,7 @@ def test_device_more_than_2_32_runs(passes):
     from flrl.device import RLDevice, gen
     n = (1 << 32) + (1 << 28) + 12345
     x = gen("u8", n, 77)
-    d = RLDevice(n, form=passes)
+    d = RLDevice(n)
     d.encode(x)
     R = d.runs()
     assert d.error() == 0

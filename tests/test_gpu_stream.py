@@ -327,6 +327,91 @@ def test_cli_streamed_error_keeps_existing_output(cli_path, tmp_path):
     assert sorted(p.name for p in tmp_path.iterdir()) == ["bad.fl", "out"]
 
 
+@pytest.fixture
+def ro_dir(tmp_path):
+    """A read-only directory (mode 0555) holding a writable existing output
+    'out'; OutFile can create no temporary there and writes in place. Root
+    ignores directory permissions, so the case only exists for other users
+    (the GPU box runs tests as an ordinary user)."""
+    if os.geteuid() == 0:
+        pytest.skip("root bypasses directory permissions")
+    d = tmp_path / "ro"
+    d.mkdir()
+    out = d / "out"
+    out.write_bytes(b"old")
+    out.chmod(0o666)
+    d.chmod(0o555)
+    yield d
+    d.chmod(0o755)
+
+
+@pytest.mark.parametrize("method", ["fl", "rl"])
+def test_cli_read_only_dir_in_place(cli_path, tmp_path, ro_dir, method):
+    """the RL side file used to be created next to the output after
+    the output was truncated in place, so `c rl` into a read-only directory
+    destroyed the existing output and failed. It now falls back to $TMPDIR and
+    is created first: both methods succeed and round-trip."""
+    data = _input("mixed", (2 << 20) + 5, 12)
+    src, back = tmp_path / "in", tmp_path / "back"
+    data.tofile(src)
+    env = dict(os.environ, FLRL_CHUNK_BYTES=str(1 << 19), FLRL_WORKERS="2", TMPDIR=str(tmp_path))
+    out = ro_dir / "out"
+    r = subprocess.run([cli_path, "c", method, str(src), str(out)], env=env, capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    if method == "fl":
+        assert out.read_bytes() == _oracle_file(data)
+    r = subprocess.run([cli_path, "d", method, str(out), str(back)], env=env, capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    assert back.read_bytes() == data.tobytes()
+    assert [p.name for p in ro_dir.iterdir()] == ["out"]
+
+
+def test_cli_read_only_dir_failures(cli_path, tmp_path, ro_dir):
+    """Failures before the in-place open leave the output alone: a missing
+    input, and the output being the input (never truncated while read). A
+    failure after it leaves the output truncated or partial, as documented in
+    flrl_outfile.hpp (the reference's fopen "wb" does the same)."""
+    out = ro_dir / "out"
+    for m in ("fl", "rl"):
+        r = subprocess.run([cli_path, "c", m, str(tmp_path / "missing"), str(out)], capture_output=True, text=True)
+        assert r.returncode == 2 and "[ERROR]" in r.stderr
+        assert out.read_bytes() == b"old"
+        r = subprocess.run([cli_path, "c", m, str(out), str(out)], capture_output=True, text=True)
+        assert r.returncode == 2 and "[ERROR]" in r.stderr
+        assert out.read_bytes() == b"old"
+    data = _input("mixed", (3 << 20) + 1, 13)
+    src = tmp_path / "in"
+    data.tofile(src)
+    flrl.debug_fail_chunk(1)
+    try:
+        with pytest.raises(flrl.FLRLError):
+            flrl.rl_compress_file(str(src), str(out), 2, 1 << 20)
+    finally:
+        flrl.debug_fail_chunk(-1)
+    assert out.read_bytes() != b"old"  # truncated at open: the documented exception
+    flrl.rl_compress_file(str(src), str(out), 2, 1 << 20)  # and the next call works
+    back = tmp_path / "back"
+    flrl.rl_decompress_file(str(out), str(back), 2, 1 << 20)
+    assert back.read_bytes() == data.tobytes()
+    assert [p.name for p in ro_dir.iterdir()] == ["out"]
+
+
+def test_alternating_host_calls_keep_their_staging():
+    """the idle-pool cap (1 GiB) was just below one compress set
+    plus one decompress set of all 8 pipelines (~1028 MiB), so every call of an
+    alternating compress/decompress loop evicted and re-allocated a 64 MiB set.
+    With the cap sized from the sets, the idle pool holds all 16 afterwards."""
+    import flrl
+    a = oracle.gen("lo4", (128 << 20) + 3, 21)  # 9 chunks: every pipeline busy
+    flrl.release_staging()
+    for _ in range(3):
+        c = flrl.fl_compress(a)
+        assert np.array_equal(flrl.fl_decompress(a.size, c.bits, c.values), a)
+    freed = flrl.release_staging()
+    # 2 directions x 8 pipelines x 2 slots x (two 16 MiB buffers + the bits)
+    assert freed >= 2 * 8 * 2 * (32 << 20), freed
+
+
 def test_release_staging_frees_idle_sets():
     """The host API keeps its pinned staging between calls (bounded); releasing
     it frees the idle sets, and the next call allocates afresh."""
