@@ -51,6 +51,7 @@ constexpr int kRlThreads = FLRL_RL_THREADS;         // encode workgroup: 4 waves
 constexpr int kRlLaneBytes = 64;                    // contiguous bytes per lane (a u64 head mask)
 constexpr int kRlSub = 32768 / (64 * kRlLaneBytes); // sub-chunks per wave chunk (one look-back per tile)
 constexpr int kRlTileBytes = kRlLaneBytes * kRlThreads * kRlSub;  // 128 KiB: 4 waves x 32 KiB
+constexpr int kRlLookG = FLRL_RL_LOOKG;  // look-back granules per lane (window 64 G tiles)
 constexpr int kRlLookL = FLRL_RL_LOOKL;  // look-back lanes polled per window
 constexpr int kRlStatusStride = FLRL_RL_STATUS_STRIDE;  // status granules per tile
 constexpr size_t kRlStatusOff = FLRL_RL_STATUS_OFF;    // status array offset in the scratch
@@ -203,11 +204,12 @@ __device__ __forceinline__ void publish_seg(uint64_t *status, uint32_t tile, uin
 // slot unpublished for help_ticks (s_memrealtime, 100 MHz; kRlHelpTicks unless
 // flrl_debug_lookback_help_us sets it) is computed here instead of waited for.
 constexpr uint64_t kRlHelpTicks = 20000;  // 200 us
-template <int L, int S, class Help>
+template <int G, int L, int S, class Help>
 __device__ __forceinline__ uint64_t lookback_seg(uint64_t *status, uint32_t tile, uint64_t map,
                                                  Ctrl *ctrl, uint64_t help_ticks, Help &&help)
 {
-    static_assert(L >= 1 && L <= kWave, "window of L lanes");
+    static_assert(L >= 1 && L <= kWave && (G == 1 || L == kWave), "window of L lanes x G granules");
+    static_assert((uint64_t)kWave * G * kRlTileBytes < (1ull << 26), "window maps within the 26-bit fields");
     const int lane = threadIdx.x & (kWave - 1);
     const uint64_t kPay = (1ull << 62) - 1;
     if (tile == 0)
@@ -220,24 +222,53 @@ __device__ __forceinline__ uint64_t lookback_seg(uint64_t *status, uint32_t tile
     uint32_t spins = 0, rounds = 0;
     for (;;) {
         ++rounds;
-        const int64_t idx = j - (int64_t)lane;
-        uint64_t ov = 0;  // this lane's slot as computed by help (0: none)
+        const int64_t idx = j - (int64_t)lane * G;  // the lane's newest slot; k = 0..G-1 older
+        uint64_t ov[G];  // this lane's slots as computed by help (0: none)
+#pragma unroll
+        for (int k = 0; k < G; ++k)
+            ov[k] = 0;
         uint64_t t0 = 0;
         bool helping = false;
         uint64_t m;
         bool has_p;
         for (;;) {
-            uint64_t s = lane >= L   ? (kFlagA | sm_nonat(0))
-                         : idx >= 0 ? granule_load(&status[idx * S])
-                                    : (kFlagP | sm_const(0, 0));
-            if ((s >> 62) == 0 && ov != 0)
-                s = ov;
-            // ready if nothing up to the window's nearest P is unpublished
-            const uint32_t f = (uint32_t)(s >> 62);
-            has_p = f == 2;
-            m = has_p ? sm_compose(sm_const(sm_h(s), sm_c(s)), sm_nonat(0)) : sm_compose(s & kPay, sm_nonat(0));
+            uint64_t sv[G];
+#pragma unroll
+            for (int k = 0; k < G; ++k) {
+                sv[k] = lane >= L       ? (kFlagA | sm_nonat(0))
+                        : idx - k >= 0 ? granule_load(&status[(idx - k) * S])
+                                       : (kFlagP | sm_const(0, 0));
+                if ((sv[k] >> 62) == 0 && ov[k] != 0)
+                    sv[k] = ov[k];
+            }
+            // lane-local, newest slot first: ready if nothing up to the lane's
+            // nearest P is unpublished; kp = that P (G - 1: none), kbad = the
+            // newest unpublished slot before it
+            has_p = false;
+            bool ok = true;
+            int kp = G - 1, kbad = 0;
+#pragma unroll
+            for (int k = 0; k < G; ++k) {
+                if (!has_p) {
+                    const uint32_t f = (uint32_t)(sv[k] >> 62);
+                    if (f == 0 && ok) {
+                        ok = false;
+                        kbad = k;
+                    }
+                    if (f == 2) {
+                        has_p = true;
+                        kp = k;
+                    }
+                }
+            }
+            // the lane's map, oldest needed slot first (identity: no-nat L 0)
+            m = sm_nonat(0);
+#pragma unroll
+            for (int k = G - 1; k >= 0; --k)
+                if (k <= kp)
+                    m = sm_compose(m, (sv[k] >> 62) == 2 ? sm_const(sm_h(sv[k]), sm_c(sv[k])) : (sv[k] & kPay));
             const unsigned long long pm = __ballot(has_p);
-            const unsigned long long bad = __ballot(f == 0);
+            const unsigned long long bad = __ballot(!ok);
             const unsigned long long upto = pm ? ((pm & (~pm + 1)) << 1) - 1 : ~0ull;
             if ((bad & upto) == 0)
                 break;
@@ -253,11 +284,14 @@ __device__ __forceinline__ uint64_t lookback_seg(uint64_t *status, uint32_t tile
                 if (now - t0 >= help_ticks)
                     helping = true;
             }
-            if (helping) {  // the oldest unpublished slot the window needs (uniform)
+            if (helping) {  // an unpublished slot the window needs (uniform: lane l, slot kl)
                 const int l = __ffsll(bad & upto) - 1;
-                const uint64_t hm = help((uint32_t)(j - l));
-                if (lane == l)
-                    ov = kFlagA | hm;
+                const int kl = __builtin_amdgcn_readlane(kbad, l);
+                const uint64_t hm = help((uint32_t)(j - (int64_t)l * G - kl));
+#pragma unroll
+                for (int k = 0; k < G; ++k)
+                    if (lane == l && k == kl)
+                        ov[k] = kFlagA | hm;
                 continue;
             }
             __builtin_amdgcn_s_sleep(1);
@@ -308,7 +342,7 @@ __device__ __forceinline__ uint64_t lookback_seg(uint64_t *status, uint32_t tile
         } else {
             acc_a = sm_a(win) + acc_a;
         }
-        j -= (int64_t)L;
+        j -= (int64_t)L * G;
     }
 }
 
@@ -976,7 +1010,7 @@ __global__ __launch_bounds__(T, kRlWavesPerSimd) void rl_encode_wave_kernel(  //
         FLRL_RL_TRACE(tile, 2);
         // decoupled fallback: a predecessor tile's map from its input
         auto help = [&](uint32_t t) -> uint64_t { return rl_tile_map_slow<Wv::TBT>(in, n, t); };
-        uint64_t st = lookback_seg<kRlLookL, kRlStatusStride>(status, tile, tmap, ctrl, help_ticks, help);
+        uint64_t st = lookback_seg<kRlLookG, kRlLookL, kRlStatusStride>(status, tile, tmap, ctrl, help_ticks, help);
         FLRL_RL_TRACE(tile, 3);
         if (V.lane == 0) {
 #pragma unroll

@@ -59,15 +59,24 @@ __global__ void put_u64_kernel(uint64_t *p, uint64_t v)
         *p = v;
 }
 
+__global__ void put_pair_kernel(uint64_t *p, uint64_t a, uint64_t b)
+{
+    if (threadIdx.x == 0 && blockIdx.x == 0) {
+        p[0] = a;
+        p[1] = b;
+    }
+}
+
 // Each thread owns one local shard: its record from the all-gathered slots
 // (shard_record, flrl_shard_layout.hpp: the layout the CPU tests check through
-// flrl_shard_scan); a ragged shard before the last raises FLRL_E_ARG in that
-// shard's scratch error word.
+// flrl_shard_scan); a ragged shard before the last, or any shard whose rank
+// failed, raises FLRL_E_ARG in that shard's scratch error word. A null sizes
+// or ctrl pointer (a rank that failed on its own arguments) is skipped.
 __global__ __launch_bounds__(kWave) void size_scan_kernel(const uint64_t *gather, uint32_t nshards,
                                                           uint32_t ndev, uint32_t S, LocalOuts outs)
 {
     for (uint32_t i = threadIdx.x; i < outs.count; i += blockDim.x)
-        if (!shard_record(gather, nshards, ndev, S, outs.index[i], outs.sizes[i]))
+        if (shard_record(gather, nshards, ndev, S, outs.index[i], outs.sizes[i]) && outs.ctrl[i])
             raise_error(outs.ctrl[i], FLRL_E_ARG);
 }
 
@@ -78,6 +87,7 @@ struct Dev {
     hipEvent_t cdone = nullptr;
     uint64_t *gather = nullptr;
     size_t gather_cap = 0;          // u64 entries
+    uint64_t *red = nullptr;        // 4 u64: flrl_fl_compress_rank's {size, failed} all-reduce
     std::vector<hipEvent_t> ev;     // per local shard slot
 };
 
@@ -105,6 +115,8 @@ int dev_setup(Dev &d, size_t gather_entries)
         return set_error(FLRL_E_HIP, "hipStreamCreate failed on device %d", d.id);
     if (!d.cdone && hipEventCreateWithFlags(&d.cdone, hipEventDisableTiming) != hipSuccess)
         return set_error(FLRL_E_HIP, "hipEventCreate failed on device %d", d.id);
+    if (!d.red && hipMalloc(&d.red, 4 * sizeof(uint64_t)) != hipSuccess)
+        return set_error(FLRL_E_NOMEM, "Cannot allocate memory (device %d)", d.id);
     if (gather_entries > d.gather_cap) {
         if (d.gather) {  // the previous call's exchange may still read it
             (void)hipStreamSynchronize(d.cstream);
@@ -131,6 +143,8 @@ void dev_release(Dev &d, bool destroy_nccl)
         (void)hipStreamSynchronize(d.cstream);
     if (d.gather)
         (void)hipFree(d.gather);
+    if (d.red)
+        (void)hipFree(d.red);
     for (hipEvent_t e : d.ev)
         (void)hipEventDestroy(e);
     if (d.cdone)
@@ -339,13 +353,18 @@ extern "C" size_t flrl_shard_slot(int shard, int nshards, int ndev)
 
 extern "C" uint64_t flrl_shard_size_word(size_t n) { return shard_f_word(n); }
 
+extern "C" uint64_t flrl_shard_failed_word(void) { return shard_failed_word(); }
+
 extern "C" int flrl_shard_scan(const uint64_t *gather, int nshards, int ndev, int shard, uint64_t *rec)
 {
     clear_error();
     if (!gather || !rec || nshards <= 0 || ndev <= 0 || shard < 0 || shard >= nshards)
         return set_error(FLRL_E_ARG, "flrl_shard_scan: shard %d of %d on %d devices", shard, nshards, ndev);
     const uint32_t S = (uint32_t)div_up((size_t)nshards, (size_t)ndev);
-    if (!shard_record(gather, (uint32_t)nshards, (uint32_t)ndev, S, (uint32_t)shard, rec))
+    const uint32_t bad = shard_record(gather, (uint32_t)nshards, (uint32_t)ndev, S, (uint32_t)shard, rec);
+    if (bad & kRecFailed)
+        return set_error(FLRL_E_ARG, "flrl_shard_scan: a shard's rank failed before the exchange");
+    if (bad & kRecRagged)
         return set_error(FLRL_E_ARG, "flrl_shard_scan: a shard before the last is not a multiple of %d bytes",
                          kFrame);
     return FLRL_OK;
@@ -353,44 +372,80 @@ extern "C" int flrl_shard_scan(const uint64_t *gather, int nshards, int ndev, in
 
 // ---- device-resident encode + exchange ------------------------------------
 
-extern "C" int flrl_fl_encode_rank(flrl_comm *c, const uint8_t *d_in, size_t n, uint8_t *d_bits,
-                                   uint8_t *d_values, uint64_t *d_sizes, void *d_scratch,
-                                   size_t scratch_bytes, void *stream)
+namespace {
+
+// flrl_fl_encode_rank's body. `local` != FLRL_OK: this rank has already failed
+// (flrl_fl_compress_rank: an allocation or upload), so it joins the exchange
+// with a failed slot instead of encoding. A local argument failure of the
+// encode does the same. Either way the all-gather runs on every rank, every
+// peer's scan raises FLRL_E_ARG, and this rank returns its own error; only a
+// comm that cannot take part at all (null, multi-device) returns before it.
+int encode_rank_impl(flrl_comm *c, const uint8_t *d_in, size_t n, uint8_t *d_bits, uint8_t *d_values,
+                     uint64_t *d_sizes, void *d_scratch, size_t scratch_bytes, void *stream, int local)
 {
-    clear_error();
-    if (!c || !d_sizes)
-        return set_error(FLRL_E_ARG, "flrl_fl_encode_rank: null comm/sizes");
+    if (!c)
+        return set_error(FLRL_E_ARG, "flrl_fl_encode_rank: null comm");
     if (c->dev.size() != 1)
         return set_error(FLRL_E_ARG,
                          "flrl_fl_encode_rank: comm drives %zu devices (use flrl_fl_encode_sharded)",
                          c->dev.size());
     std::lock_guard<std::mutex> g(c->mu);
     Dev &d = c->dev[0];
-    if (current_device() != d.id)
-        return set_error(FLRL_E_ARG, "flrl_fl_encode_rank: current device %d, comm on device %d",
-                         current_device(), d.id);
+    const int prev = current_device();
     hipStream_t s = static_cast<hipStream_t>(stream);
+    if (local == FLRL_OK && prev != d.id)
+        local = set_error(FLRL_E_ARG, "flrl_fl_encode_rank: current device %d, comm on device %d", prev, d.id);
+    if (local == FLRL_OK && !d_sizes)
+        local = set_error(FLRL_E_ARG, "flrl_fl_encode_rank: null sizes");
+    if (local != FLRL_OK) {  // the caller's stream may be unusable: the comm's own
+        s = d.cstream;
+        if (hipSetDevice(d.id) != hipSuccess)
+            return local;
+    }
     // the previous call's scan may still read the gather array on another stream
-    FLRL_HIP(hipStreamWaitEvent(s, d.cdone, 0));
+    if (hipStreamWaitEvent(s, d.cdone, 0) != hipSuccess) {
+        (void)hipSetDevice(prev);
+        return local ? local : set_error(FLRL_E_HIP, "flrl_fl_encode_rank: event wait failed");
+    }
     uint64_t *slot = d.gather + shard_slot((uint64_t)c->rank, (uint64_t)c->nranks, 1);
-    hipLaunchKernelGGL(put_u64_kernel, dim3(1), dim3(kWave), 0, s, slot, shard_f_word(n));
-    FLRL_HIP(hipGetLastError());
-    int rc = flrl_fl_encode_device(d_in, n, d_bits, d_values, slot + 1, d_scratch, scratch_bytes, stream);
-    if (rc)
-        return rc;
+    if (local == FLRL_OK) {
+        hipLaunchKernelGGL(put_u64_kernel, dim3(1), dim3(kWave), 0, s, slot, shard_f_word(n));
+        if (hipGetLastError() != hipSuccess)
+            local = set_error(FLRL_E_HIP, "flrl_fl_encode_rank: launch failed");
+        else
+            local = flrl_fl_encode_device(d_in, n, d_bits, d_values, slot + 1, d_scratch, scratch_bytes, s);
+        // on failure the failed pair follows the F word on the same stream (the
+        // encode's argument checks precede every launch of it)
+    }
+    if (local != FLRL_OK)
+        hipLaunchKernelGGL(put_pair_kernel, dim3(1), dim3(kWave), 0, s, slot, shard_failed_word(), (uint64_t)0);
     const ncclResult_t r = ncclAllGather(slot, d.gather, 2, ncclUint64, d.nccl, s);  // in place
-    if (r != ncclSuccess)
-        return rccl_error(r, "ncclAllGather");
+    if (r != ncclSuccess) {
+        (void)hipSetDevice(prev);
+        return local ? local : rccl_error(r, "ncclAllGather");
+    }
     LocalOuts outs{};
     outs.count = 1;
     outs.index[0] = (uint32_t)c->rank;
-    outs.sizes[0] = d_sizes;
-    outs.ctrl[0] = static_cast<Ctrl *>(d_scratch);
+    outs.sizes[0] = d_sizes;  // the failing rank's record too, when it gave one
+    outs.ctrl[0] = local == FLRL_OK ? static_cast<Ctrl *>(d_scratch) : nullptr;
     hipLaunchKernelGGL(size_scan_kernel, dim3(1), dim3(kWave), 0, s, d.gather, (uint32_t)c->nranks,
                        (uint32_t)c->nranks, 1u, outs);
-    FLRL_HIP(hipGetLastError());
-    FLRL_HIP(hipEventRecord(d.cdone, s));
-    return FLRL_OK;
+    const bool ok = hipGetLastError() == hipSuccess && hipEventRecord(d.cdone, s) == hipSuccess;
+    (void)hipSetDevice(prev);
+    if (local != FLRL_OK)
+        return local;
+    return ok ? FLRL_OK : set_error(FLRL_E_HIP, "flrl_fl_encode_rank: size scan failed");
+}
+
+}  // namespace
+
+extern "C" int flrl_fl_encode_rank(flrl_comm *c, const uint8_t *d_in, size_t n, uint8_t *d_bits,
+                                   uint8_t *d_values, uint64_t *d_sizes, void *d_scratch,
+                                   size_t scratch_bytes, void *stream)
+{
+    clear_error();
+    return encode_rank_impl(c, d_in, n, d_bits, d_values, d_sizes, d_scratch, scratch_bytes, stream, FLRL_OK);
 }
 
 extern "C" int flrl_fl_encode_sharded(flrl_comm *c, int nshards, const uint8_t *const *d_in,
@@ -694,51 +749,81 @@ extern "C" int flrl_fl_compress_rank(flrl_comm *c, const uint8_t *data, size_t s
     if (c->dev.size() != 1)
         return set_error(FLRL_E_ARG, "flrl_fl_compress_rank: needs a per-rank communicator");
     const int prev = current_device();
+    Dev &dv = c->dev[0];
+    // Collective on errors: a rank that fails anywhere
+    // still completes (1) the exchange, with a failed slot, and (2) the
+    // all-reduce of {size, failed}; (3) the payload send/recv runs only when no
+    // rank failed, so no peer ever waits in a collective this rank skipped.
     ShardBufs b;
-    int rc = b.alloc(c->dev[0].id, size);
+    int rc = b.alloc(dv.id, size);
     if (rc == FLRL_OK && size &&
         hipMemcpyAsync(b.in, data, size, hipMemcpyHostToDevice, b.s) != hipSuccess)
         rc = set_error(FLRL_E_HIP, "flrl_fl_compress_rank: upload failed");
-    if (rc == FLRL_OK)
-        rc = flrl_fl_encode_rank(c, b.in, size, b.bits, b.vals, b.sizes, b.scr, b.scr_b, b.s);
+    // (1) encode + exchange; a failed rank joins with a failed slot
+    {
+        const int e = encode_rank_impl(c, b.in, size, b.bits, b.vals, rc == FLRL_OK ? b.sizes : nullptr, b.scr,
+                                       b.scr_b, b.s ? b.s : dv.cstream, rc);
+        if (rc == FLRL_OK)
+            rc = e;
+    }
+    const bool rcl_broken = rc == FLRL_E_RCCL;  // the comm itself failed: no further collectives
     const size_t R = (size_t)c->nranks;
     std::vector<uint64_t> all(2 * R);
     uint64_t rec[FLRL_SZ_COUNT] = {0};
     if (rc == FLRL_OK) {
         std::lock_guard<std::mutex> g(c->mu);
         if (hipMemcpyAsync(rec, b.sizes, sizeof(rec), hipMemcpyDeviceToHost, b.s) != hipSuccess ||
-            hipMemcpyAsync(all.data(), c->dev[0].gather, 16 * R, hipMemcpyDeviceToHost, b.s) != hipSuccess ||
+            hipMemcpyAsync(all.data(), dv.gather, 16 * R, hipMemcpyDeviceToHost, b.s) != hipSuccess ||
             hipStreamSynchronize(b.s) != hipSuccess)
             rc = set_error(FLRL_E_HIP, "flrl_fl_compress_rank: size read-back failed");
     }
     if (rc == FLRL_OK)
-        rc = read_error(b, (size_t)c->rank);
-    // the whole input's size (the reference all-gathers inputSize, fl_gpu.cu:105)
-    uint64_t total_n = 0;
-    if (rc == FLRL_OK) {
-        std::lock_guard<std::mutex> g(c->mu);
-        uint64_t *d_n = b.sizes + FLRL_SZ_COUNT;  // spare u64s of the sizes block
-        const uint64_t mine = size;
-        ncclResult_t r1;
-        if (hipMemcpyAsync(d_n, &mine, 8, hipMemcpyHostToDevice, b.s) != hipSuccess)
-            rc = set_error(FLRL_E_HIP, "flrl_fl_compress_rank: upload failed");
-        else if ((r1 = ncclAllReduce(d_n, d_n + 1, 1, ncclUint64, ncclSum, c->dev[0].nccl, b.s)) != ncclSuccess)
-            rc = rccl_error(r1, "ncclAllReduce");
-        else if (hipMemcpyAsync(&total_n, d_n + 1, 8, hipMemcpyDeviceToHost, b.s) != hipSuccess ||
-                 hipStreamSynchronize(b.s) != hipSuccess)
-            rc = set_error(FLRL_E_HIP, "flrl_fl_compress_rank: size read-back failed");
-    }
-    // gather the payloads to rank 0 (the reference's rank-0 merge, fl_gpu.cu:144-238,
-    // without padding or broadcasting them to every rank)
+        rc = read_error(b, (size_t)c->rank);  // (a failed peer's slot raised FLRL_E_ARG here)
+    // rank 0's merge buffer before the all-reduce, so its failure is reported in it
     uint8_t *d_all = nullptr;
     const uint64_t F = rec[FLRL_SZ_F_TOTAL], V = rec[FLRL_SZ_V_TOTAL];
-    if (rc == FLRL_OK && c->rank == 0 && hipMalloc(&d_all, (F + V) ? F + V : 16) != hipSuccess)
-        rc = set_error(FLRL_E_NOMEM, "Cannot allocate memory (device)");
-    // an error on one rank leaves the others waiting in ncclRecv/ncclSend, as
-    // in the reference; the per-rank caller aborts the job on error
-    if (rc == FLRL_OK) {
+    if (rc == FLRL_OK && c->rank == 0) {
+        (void)hipSetDevice(dv.id);
+        if (hipMalloc(&d_all, (F + V) ? F + V : 16) != hipSuccess) {
+            d_all = nullptr;
+            rc = set_error(FLRL_E_NOMEM, "Cannot allocate memory (device)");
+        }
+    }
+    // (2) {whole input size (the reference all-gathers inputSize, fl_gpu.cu:105),
+    // ranks that failed}, summed over the ranks on the comm's own buffer/stream
+    uint64_t total_n = 0, failed = 0;
+    if (!rcl_broken) {
         std::lock_guard<std::mutex> g(c->mu);
-        ncclComm_t nc = c->dev[0].nccl;
+        (void)hipSetDevice(dv.id);
+        const uint64_t mine[2] = {size, rc == FLRL_OK ? 0ull : 1ull};
+        uint64_t sum[2] = {0, 1};
+        ncclResult_t r1 = ncclSuccess;
+        if (hipStreamWaitEvent(dv.cstream, dv.cdone, 0) != hipSuccess ||
+            hipMemcpyAsync(dv.red, mine, sizeof(mine), hipMemcpyHostToDevice, dv.cstream) != hipSuccess) {
+            // cannot stage our word: still take part, with whatever the buffer
+            // holds, and count this rank as failed below
+            if (rc == FLRL_OK)
+                rc = set_error(FLRL_E_HIP, "flrl_fl_compress_rank: upload failed");
+        }
+        if ((r1 = ncclAllReduce(dv.red, dv.red + 2, 2, ncclUint64, ncclSum, dv.nccl, dv.cstream)) != ncclSuccess) {
+            if (rc == FLRL_OK)
+                rc = rccl_error(r1, "ncclAllReduce");
+        } else if (hipMemcpyAsync(sum, dv.red + 2, sizeof(sum), hipMemcpyDeviceToHost, dv.cstream) != hipSuccess ||
+                   hipStreamSynchronize(dv.cstream) != hipSuccess) {
+            if (rc == FLRL_OK)
+                rc = set_error(FLRL_E_HIP, "flrl_fl_compress_rank: size read-back failed");
+        }
+        total_n = sum[0];
+        failed = sum[1];
+        if (rc == FLRL_OK && failed)
+            rc = set_error(FLRL_E_ARG, "flrl_fl_compress_rank: %llu rank(s) failed", (unsigned long long)failed);
+    }
+    // (3) the payloads to rank 0 (the reference's rank-0 merge, fl_gpu.cu:144-238,
+    // without padding or broadcasting them to every rank): only when every rank
+    // reported success in (2), so all ranks take this branch or none
+    if (rc == FLRL_OK && failed == 0 && !rcl_broken) {
+        std::lock_guard<std::mutex> g(c->mu);
+        ncclComm_t nc = dv.nccl;
         ncclResult_t r1 = ncclGroupStart();
         if (c->rank == 0) {
             for (size_t q = 0; q < R && r1 == ncclSuccess; ++q) {

@@ -14,6 +14,10 @@
 //    number of 128-byte frames; only the last shard may be ragged, otherwise
 //    its successors' frames would start mid-frame and the concatenation would
 //    no longer equal the whole-input encode;
+//  * a shard whose rank failed locally (a bad argument, an allocation) still
+//    joins the exchange, with a "failed" flag (bit 62) in its F word: every
+//    rank's scan then reports FLRL_E_ARG, where returning before the
+//    collective would leave every peer waiting in it;
 //  * the record of shard `me` (FLRL_SZ_*): its F and V, the exclusive prefix
 //    of F and V over shards 0..me-1 in shard order, and the totals.
 #pragma once
@@ -31,6 +35,12 @@
 namespace flrl {
 
 constexpr uint64_t kRaggedBit = 1ull << 63;
+constexpr uint64_t kFailedBit = 1ull << 62;
+constexpr uint64_t kShardFlags = kRaggedBit | kFailedBit;
+
+// shard_record's verdict bits
+constexpr uint32_t kRecRagged = 1;  // a shard before the last is not whole frames
+constexpr uint32_t kRecFailed = 2;  // some shard's rank failed locally
 
 FLRL_HD inline void shard_range(uint64_t n, uint64_t P, uint64_t r, uint64_t *start, uint64_t *len)
 {
@@ -50,19 +60,25 @@ FLRL_HD inline uint64_t shard_f_word(uint64_t n)
     return ((n + FLRL_FRAME_LENGTH - 1) / FLRL_FRAME_LENGTH) | (n % FLRL_FRAME_LENGTH ? kRaggedBit : 0);
 }
 
-// Record of shard `me` from the all-gathered slots. Returns false when a shard
-// other than the last is ragged (the record is still filled).
-FLRL_HD inline bool shard_record(const uint64_t *gather, uint32_t nshards, uint32_t ndev, uint32_t S,
-                                 uint32_t me, uint64_t *rec)
+// The F word (with V = 0) of a shard whose rank failed before its encode.
+FLRL_HD inline uint64_t shard_failed_word() { return kFailedBit; }
+
+// Record of shard `me` from the all-gathered slots (filled in every case; rec
+// may be null). Returns 0, or kRecRagged / kRecFailed bits: a shard other than
+// the last is ragged, or some shard's rank failed.
+FLRL_HD inline uint32_t shard_record(const uint64_t *gather, uint32_t nshards, uint32_t ndev, uint32_t S,
+                                     uint32_t me, uint64_t *rec)
 {
     uint64_t F = 0, V = 0, Fo = 0, Vo = 0, Fr = 0, Vr = 0;
-    bool ok = true;
+    uint32_t bad = 0;
     for (uint32_t r = 0; r < nshards; ++r) {
         const uint64_t *g = gather + shard_slot(r, ndev, S);
         const uint64_t fw = g[0], v = g[1];
-        const uint64_t f = fw & ~kRaggedBit;
+        const uint64_t f = fw & ~kShardFlags;
         if ((fw & kRaggedBit) && r + 1 != nshards)
-            ok = false;
+            bad |= kRecRagged;
+        if (fw & kFailedBit)
+            bad |= kRecFailed;
         if (r == me) {
             Fo = F;
             Vo = V;
@@ -72,13 +88,15 @@ FLRL_HD inline bool shard_record(const uint64_t *gather, uint32_t nshards, uint3
         F += f;
         V += v;
     }
-    rec[FLRL_SZ_F] = Fr;
-    rec[FLRL_SZ_V] = Vr;
-    rec[FLRL_SZ_F_OFF] = Fo;
-    rec[FLRL_SZ_V_OFF] = Vo;
-    rec[FLRL_SZ_F_TOTAL] = F;
-    rec[FLRL_SZ_V_TOTAL] = V;
-    return ok;
+    if (rec) {
+        rec[FLRL_SZ_F] = Fr;
+        rec[FLRL_SZ_V] = Vr;
+        rec[FLRL_SZ_F_OFF] = Fo;
+        rec[FLRL_SZ_V_OFF] = Vo;
+        rec[FLRL_SZ_F_TOTAL] = F;
+        rec[FLRL_SZ_V_TOTAL] = V;
+    }
+    return bad;
 }
 
 }  // namespace flrl

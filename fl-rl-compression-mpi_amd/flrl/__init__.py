@@ -139,6 +139,7 @@ _sig("flrl_shard_range", ctypes.c_int, _sz, ctypes.c_int, ctypes.c_int, ctypes.P
      ctypes.POINTER(_sz))
 _sig("flrl_shard_slot", _sz, ctypes.c_int, ctypes.c_int, ctypes.c_int)
 _sig("flrl_shard_size_word", _u64, _sz)
+_sig("flrl_shard_failed_word", _u64)
 _sig("flrl_shard_scan", ctypes.c_int, _vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, _vp)
 _sig("flrl_fl_encode_sharded", ctypes.c_int, _vp, ctypes.c_int, _pp, ctypes.POINTER(_sz), _pp, _pp,
      _pp, _pp, ctypes.POINTER(_sz), _pp)
@@ -246,6 +247,12 @@ def shard_slot(shard: int, nshards: int, ndev: int) -> int:
 def shard_size_word(n: int) -> int:
     """The F word a shard of n bytes puts into its slot (bit 63: ragged)."""
     return int(_lib.flrl_shard_size_word(n))
+
+
+def shard_failed_word() -> int:
+    """The F word (V = 0) a rank that failed locally puts into its slot, so that
+    every rank's scan reports FLRL_E_ARG instead of peers waiting forever."""
+    return int(_lib.flrl_shard_failed_word())
 
 
 def shard_scan(gather: np.ndarray, nshards: int, ndev: int, shard: int) -> list[int]:

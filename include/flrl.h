@@ -144,7 +144,12 @@ int flrl_comm_query(const flrl_comm *c, int *nranks, int *rank, int *ndev);
  * `stream` with no host synchronisation. Every rank of the comm must call it
  * (collective). Shards of ranks 0..nranks-2 must be multiples of 128 bytes:
  * otherwise every rank's scratch error word reads FLRL_E_ARG after the
- * exchange. The device half of gpuNCCLCompress (fl_gpu.cu:76-143). */
+ * exchange. A rank whose arguments fail locally (null or undersized scratch,
+ * misaligned buffers, the current device not the comm's) still joins the
+ * exchange with a failed slot (flrl_shard_failed_word) and returns its own
+ * error code; every other rank's scratch error word then reads FLRL_E_ARG
+ * (instead of waiting forever in the all-gather, as gpuNCCLCompress's peers
+ * would). The device half of gpuNCCLCompress (fl_gpu.cu:76-143). */
 int flrl_fl_encode_rank(flrl_comm *c, const uint8_t *d_in, size_t n, uint8_t *d_bits,
                         uint8_t *d_values, uint64_t *d_sizes, void *d_scratch,
                         size_t scratch_bytes, void *stream);
@@ -153,7 +158,11 @@ int flrl_fl_encode_rank(flrl_comm *c, const uint8_t *d_in, size_t n, uint8_t *d_
  * (fl_gpu.cuh:16): each rank passes its own shard (loadFileMpi, file_io.cu:28-71);
  * rank 0 receives the merged whole-input result (input_size = sum of the
  * ranks' sizes), the other ranks an empty flrl_fl_buf — the reference's rank-0
- * merge (fl_gpu.cu:196-238). Payloads travel ncclSend/ncclRecv to rank 0 only. */
+ * merge (fl_gpu.cu:196-238). Payloads travel ncclSend/ncclRecv to rank 0 only.
+ * Collective on errors too: a rank that fails (allocation, upload, device
+ * error, rank 0's merge buffer) still completes the exchange and an all-reduce
+ * of {size, failed}, so every rank returns an error and none waits in the
+ * payload send/recv. */
 int flrl_fl_compress_rank(flrl_comm *c, const uint8_t *data, size_t size, flrl_fl_buf *out);
 
 /* The exchange's layout, host-callable (the device scan runs the same code,
@@ -167,12 +176,15 @@ int flrl_fl_compress_rank(flrl_comm *c, const uint8_t *data, size_t size, flrl_f
  *    one process per GPU: ndev = nshards); (size_t)-1 for bad arguments.
  *  flrl_shard_size_word: the F word a shard of n bytes contributes (ceil(n/128),
  *    bit 63 set when n is not a multiple of 128).
+ *  flrl_shard_failed_word: the F word (bit 62; V = 0) of a shard whose rank
+ *    failed locally but still joins the exchange.
  *  flrl_shard_scan: shard's record (u64[FLRL_SZ_COUNT]) from the gathered
- *    array; FLRL_E_ARG if a shard before the last is ragged (the record is
- *    still written). */
+ *    array; FLRL_E_ARG if a shard before the last is ragged or any shard
+ *    carries the failed word (the record is still written). */
 int flrl_shard_range(size_t n, int nshards, int shard, size_t *start, size_t *length);
 size_t flrl_shard_slot(int shard, int nshards, int ndev);
 uint64_t flrl_shard_size_word(size_t n);
+uint64_t flrl_shard_failed_word(void);
 int flrl_shard_scan(const uint64_t *gather, int nshards, int ndev, int shard, uint64_t *rec);
 
 /* Single-process device-resident sharded encode (flrl_comm_init comm): shard r

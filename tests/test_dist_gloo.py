@@ -31,7 +31,7 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, n, ragged_rank, q):
+def _worker(rank, world, port, n, ragged_rank, q, failed_rank=None):
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     sys.path.insert(0, os.path.dirname(here))
@@ -51,6 +51,8 @@ def _worker(rank, world, port, n, ragged_rank, q):
         bits, values = oracle.fl_compress(whole[start:start + length])
         # the rank's slot pair, exactly as put_u64_kernel + the encode write it
         mine = np.array([fl.shard_size_word(length), values.size], dtype=np.uint64)
+        if rank == failed_rank:  # a local failure still joins the exchange (flrl_fl_encode_rank)
+            mine = np.array([fl.shard_failed_word(), 0], dtype=np.uint64)
         slot = fl.shard_slot(rank, world, world)
         gathered = torch.zeros(2 * world, dtype=torch.int64)
         dist.all_gather_into_tensor(gathered, torch.from_numpy(mine.view(np.int64)))
@@ -64,7 +66,7 @@ def _worker(rank, world, port, n, ragged_rank, q):
         parts = [None] * world
         dist.all_gather_object(parts, (rec, err, bits.tobytes(), values.tobytes()))
         if rank == 0:
-            if ragged_rank is not None:
+            if ragged_rank is not None or failed_rank is not None:
                 q.put([p[1] for p in parts])
                 return
             F, V = parts[0][0][flrl.SZ_F_TOTAL], parts[0][0][flrl.SZ_V_TOTAL]
@@ -83,11 +85,12 @@ def _worker(rank, world, port, n, ragged_rank, q):
         dist.destroy_process_group()
 
 
-def _run(world, n, ragged_rank=None):
+def _run(world, n, ragged_rank=None, failed_rank=None):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, n, ragged_rank, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n, ragged_rank, q, failed_rank))
+             for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
@@ -107,6 +110,30 @@ def test_rank_exchange_flags_ragged_shard():
     """A shard before the last that is not whole frames: every rank's scan
     reports FLRL_E_ARG (on the device: each rank's scratch error word)."""
     assert _run(3, 4096, ragged_rank=0) == [flrl.E_ARG] * 3
+
+
+@pytest.mark.parametrize("world,failed", [(2, 1), (3, 0), (4, 2)])
+def test_rank_exchange_flags_failed_rank(world, failed):
+    """a rank whose encode fails locally (scratch too
+    small, misaligned buffers) no longer returns before the all-gather, which
+    left every peer waiting in it: it joins with flrl_shard_failed_word() in its
+    slot, and every rank's scan (the device size_scan_kernel runs the same
+    shard_record) reports FLRL_E_ARG."""
+    assert _run(world, 1_000_003, failed_rank=failed) == [flrl.E_ARG] * world
+
+
+def test_shard_scan_failed_word():
+    ok = np.array([flrl.shard_size_word(256), 5, flrl.shard_size_word(300), 7], dtype=np.uint64)
+    assert flrl.shard_scan(ok, 2, 2, 1) == [3, 7, 2, 5, 5, 12]
+    for bad_slot in (0, 2):
+        g = ok.copy()
+        g[bad_slot], g[bad_slot + 1] = flrl.shard_failed_word(), 0
+        for me in (0, 1):
+            with pytest.raises(flrl.FLRLError) as e:
+                flrl.shard_scan(g, 2, 2, me)
+            assert e.value.code == flrl.E_ARG and "failed" in str(e.value)
+    assert flrl.shard_failed_word() == 1 << 62
+    assert flrl.shard_failed_word() & flrl.shard_size_word(1 << 40) == 0
 
 
 def _whole_scan(F, V, r):

@@ -258,6 +258,34 @@ def test_encode_rank_record(rank_comm, golden):
                     d.values[:v].cpu().numpy().tobytes()) == g["fl_sha256"]
 
 
+def test_encode_rank_local_error_still_exchanges(rank_comm):
+    """an undersized scratch is a local argument error,
+    found before any encode launch; the rank still runs the all-gather (with a
+    failed slot, flrl_shard_failed_word) and the size scan, so its peers see
+    FLRL_E_ARG instead of waiting in the collective. On a one-rank comm: the
+    call raises FLRL_E_ARG, the scan still wrote this rank's record (the failed
+    slot reads F = V = 0), and the comm keeps working."""
+    from flrl.device import FLDevice
+    n = 1 << 20
+    x = torch.randint(0, 256, (n,), dtype=torch.uint8, device="cuda")
+    d = FLDevice(n)
+    d.rank_sizes = torch.full((8,), -1, dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()
+    with pytest.raises(flrl.FLRLError) as e:
+        rank_comm.encode_rank(x.data_ptr(), n, d.bits.data_ptr(), d.values.data_ptr(), d.rank_sizes.data_ptr(),
+                              d.scratch.data_ptr(), 64, torch.cuda.current_stream().cuda_stream)
+    assert e.value.code == flrl.E_ARG and "scratch" in str(e.value)
+    torch.cuda.synchronize()
+    assert [int(t) for t in d.rank_sizes[:flrl.SZ_COUNT].cpu()] == [0] * flrl.SZ_COUNT
+    d.encode_rank(rank_comm, x)  # the next call works
+    torch.cuda.synchronize()
+    rec = [int(t) for t in d.rank_sizes[:flrl.SZ_COUNT].cpu()]
+    v = rec[flrl.SZ_V]
+    assert rec == [n // 128, v, 0, 0, n // 128, v] and v > 0
+    assert d.error() == 0
+    assert torch.equal(d.decode(v), x)
+
+
 def test_encode_rank_rejects_sharded_comm(local_comm):
     from flrl.device import FLDevice
     if flrl.device_count() > 1:
