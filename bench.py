@@ -86,7 +86,11 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=5)
-    p.add_argument("--bytes", type=int, default=1 << 30, help="input bytes per GPU")
+    p.add_argument("--bytes", type=int, default=1 << 30, help="input bytes per GPU (weak scaling, the default)")
+    p.add_argument("--global-bytes", type=int, default=0,
+                   help="strong scaling: a FIXED total split over the N ranks by the reference shard rule "
+                        "(file_io.cu:46-51, flrl_shard_range: every shard but the last floor(B/(128N))*128 "
+                        "bytes); the line reports scaling 'strong' and value = B / step time")
     p.add_argument("--kind", default="u8", choices=["u8", "lo4", "zero"])
     p.add_argument("--seed", type=int, default=42)
     p.add_argument("--cpu-sample", type=int, default=-1,
@@ -161,6 +165,23 @@ def cpu_baseline(kind: str, seed: int, sample: int, gpu_bits, gpu_values):
         "roundtrip_ok": ok,
         "gpu_bytes_equal_oracle": same,
     }
+
+
+def rank_shard(per_gpu: int, global_bytes: int, world: int, rank: int) -> tuple[int, int, int]:
+    """(start, length, job total) of rank's input bytes. Weak scaling (the
+    default): `per_gpu` bytes per rank, rank r at r * per_gpu. Strong scaling
+    (global_bytes > 0; on_cluster.sh:18-34 splits fixed 512/2048/3124 MB files
+    over the mpirun ranks): the fixed total split by the reference shard rule
+    (file_io.cu:46-51 via flrl_shard_range), every shard but the last
+    floor(B / (128 N)) * 128 bytes, so only the last may be ragged."""
+    if global_bytes > 0:
+        if global_bytes < 128 * world:
+            raise SystemExit("--global-bytes must give every rank at least one frame")
+        start, n = flrl.shard_range(global_bytes, world, rank)
+        return start, n, global_bytes
+    if per_gpu % 128:
+        raise SystemExit("--bytes must be a multiple of 128 (frame-aligned shards for weak scaling)")
+    return rank * per_gpu, per_gpu, world * per_gpu
 
 
 def workload_ref(n: int, kind: str, world: int) -> str:
@@ -495,11 +516,10 @@ def main():
         if world > 1:
             dist.barrier()
 
-    n = args.bytes
-    if n % 128:
-        raise SystemExit("--bytes must be a multiple of 128 (frame-aligned shards for weak scaling)")
+    strong = args.global_bytes > 0
+    start, n, total = rank_shard(args.bytes, args.global_bytes, world, rank)
 
-    x = gen(args.kind, n, args.seed, word_offset=rank * n // 8, device=dev)
+    x = gen(args.kind, n, args.seed, word_offset=start // 8, device=dev)
     codec = FLDevice(n, dev)
     out = torch.empty_like(x)
     stream = torch.cuda.current_stream()
@@ -600,7 +620,7 @@ def main():
         raise SystemExit(f"device error {codec.error()} during the timed steps")
 
     ms_per_step = wall * 1e3 / args.steps
-    value = world * n / (wall / args.steps) / 1e9
+    value = total / (wall / args.steps) / 1e9
 
     # algorithmic bytes per launch: encode N+F+V, decode F+V+N
     alg = n + codec.frames + v
@@ -647,14 +667,16 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if strong else "weak",
             "vs_baseline": None,
             "dtype": "u8",
             "data": f"synthetic ({args.kind} splitmix64 seed {args.seed}, SURVEY.md §8(d), generated in HBM)",
             "config": {
-                "workload": f"FL encode+decode of {n} {args.kind} bytes per GPU ({workload_ref(n, args.kind, world)})",
+                "workload": (f"FL encode+decode of {total} {args.kind} bytes in total, split over {world} GPU(s) "
+                             f"by the reference shard rule (strong scaling)" if strong else
+                             f"FL encode+decode of {n} {args.kind} bytes per GPU ({workload_ref(n, args.kind, world)})"),
                 "bytes_per_gpu": n,
-                "global_bytes": n * world,
+                "global_bytes": total,
                 "parallelism": (f"dp{world}: 128-aligned shards, RCCL size exchange (flrl_fl_encode_rank)"
                                 if world > 1 else "single GPU"),
                 "ranks_seen": world,

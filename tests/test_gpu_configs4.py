@@ -127,3 +127,23 @@ def test_bench_configs4_section_at_one_gpu(tmp_path):
     assert c4 is not None and c4["ranks_seen"] == 1
     assert c4["size_scan_ok"] and c4["roundtrip"]
     assert line["parity"]["roundtrip"] and line["parity"]["size_scan_ok"]
+
+
+def test_bench_strong_scaling_mode_at_one_gpu(tmp_path):
+    """bench.py --global-bytes (strong scaling: a fixed total split over the
+    ranks by the reference shard rule), at N = 1 through the exchange
+    (--force-scan) on a total that is not whole frames: scaling 'strong',
+    value = total / step time, round trip and size scan green."""
+    B = (1 << 24) + 77
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1", "--steps", "3", "--warmup", "1",
+           "--global-bytes", str(B), "--force-scan", "--no-configs4", "--cpu-sample", "0",
+           "--no-north-star", "--no-rl"]
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=str(tmp_path), env=env)
+    assert p.returncode == 0, p.stderr[-3000:]
+    line = json.loads(p.stdout.strip().splitlines()[-1])
+    assert line["scaling"] == "strong"
+    assert line["config"]["global_bytes"] == B and line["config"]["bytes_per_gpu"] == B
+    assert line["parity"]["roundtrip"] and line["parity"]["size_scan_ok"]
+    assert abs(line["value"] - B / (line["ms_per_step"] * 1e-3) / 1e9) < 0.02 * line["value"] + 0.01
