@@ -504,16 +504,16 @@ struct RlWave {
     }
 
     // sub-chunk s (in pf) through the wave's LDS image; p_sub = the byte before
-    // it; pf_next: load sub-chunk s+1 into pf once this one is in LDS. Returns
-    // the sub-chunk's last byte (uniform).
-    __device__ uint32_t scan_sub(uint64_t off, int s, Sub &L, u32x4 (&pf)[NJ], uint32_t p_sub, bool pf_next) const
+    // it; s_next >= 0: load sub-chunk s_next into pf once this one is in LDS.
+    // Returns the sub-chunk's last byte (uniform).
+    __device__ uint32_t scan_sub(uint64_t off, int s, Sub &L, u32x4 (&pf)[NJ], uint32_t p_sub, int s_next) const
     {
         const uint64_t so = off + (uint64_t)s * WB;
 #pragma unroll
         for (int j = 0; j < NJ; ++j)
             *reinterpret_cast<u32x4 *>(img + j * 1024 + lane * 16) = pf[j];
-        if (pf_next)
-            load_sub(off, s + 1, pf);  // lands while this sub-chunk is scanned
+        if (s_next >= 0)
+            load_sub(off, s_next, pf);  // lands while this sub-chunk (and, PF = 2, the next) is scanned
         const uint64_t lane_off = so + o;
         L.vbl = lane_off >= n ? 0u : (n - lane_off >= LB ? (uint32_t)LB : (uint32_t)(n - lane_off));
         u32x4 x[CH];
@@ -712,11 +712,16 @@ struct RlWave {
         C.off = off;
         C.len = len;
         C.ns = (int)((len + WB - 1) / WB);
-        u32x4 pf[NJ];
+        // PF sub-chunks in flight per wave (register sets used in turn)
+        constexpr int PF = FLRL_RL_PF;
+        static_assert(PF == 1 || PF == 2, "prefetch depth");
+        u32x4 pf[PF][NJ];
         uint32_t p_sub = 0;
         C.v0 = 0;
         if (C.ns > 0) {
-            load_sub(off, 0, pf);
+            load_sub(off, 0, pf[0]);
+            if (PF == 2 && C.ns > 1)
+                load_sub(off, 1, pf[PF - 1]);
             p_sub = off > 0 ? (uint32_t)in[off - 1] : 0u;
         }
         uint32_t rel_in = kMapIdent;  // PhaseMap from the chunk start to this sub-chunk
@@ -724,9 +729,9 @@ struct RlWave {
         uint32_t K = 0;
         int nst = SUB;
         uint32_t Kst = 0, rel_st = kMapIdent;
-        for (int s = 0; s < C.ns; ++s) {
+        auto step = [&](int s, u32x4 (&buf)[NJ]) {
             Sub L;
-            const uint32_t last = scan_sub(off, s, L, pf, p_sub, s + 1 < C.ns);
+            const uint32_t last = scan_sub(off, s, L, buf, p_sub, s + PF < C.ns ? s + PF : -1);
             if (s == 0)
                 C.v0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)img[0]);
             p_sub = last;
@@ -760,6 +765,11 @@ struct RlWave {
             rel_in = pm_compose(rel_in, L.smap);
             if (nst == SUB && indep)
                 lane_runs(L, h0, h1, cr, slot);
+        };
+        for (int s = 0; s < C.ns; s += PF) {
+            step(s, pf[0]);
+            if (PF == 2 && s + 1 < C.ns)
+                step(s + 1, pf[PF - 1]);
         }
         if (nst >= C.ns) {
             nst = C.ns;
@@ -792,7 +802,7 @@ struct RlWave {
             // the previous sub-chunk's reads of the staging and the image are
             // this wave's own LDS ops: in order
             Sub L;
-            pb = scan_sub(off, s, L, pf, pb, false);
+            pb = scan_sub(off, s, L, pf, pb, -1);
 #pragma unroll
             for (int j = 0; j < NJ; ++j)
                 pf[j] = u32x4{0u, 0u, 0u, 0u};  // consumed: not live until the next load

@@ -12,7 +12,7 @@
 #if !defined(FLRL_TUNING_BUILD) &&                                                                  \
     (defined(FLRL_RL_TRACE) || defined(FLRL_RL_LB_STAT) || defined(FLRL_FL_TRACE) ||                \
      defined(FLRL_RL_THREADS) || defined(FLRL_RD_TICKET_MIN) || defined(FLRL_FL_LOOKG) || defined(FLRL_FL_LOOKL) ||\
-     defined(FLRL_FL_STATUS_STRIDE) || defined(FLRL_FL_STATUS_OFF) || defined(FLRL_RL_LOOKL) || defined(FLRL_RL_LOOKG) ||\
+     defined(FLRL_FL_STATUS_STRIDE) || defined(FLRL_FL_STATUS_OFF) || defined(FLRL_RL_LOOKL) || defined(FLRL_RL_LOOKG) || defined(FLRL_RL_PF) ||\
      defined(FLRL_RL_STATUS_STRIDE) || defined(FLRL_RL_STATUS_OFF) ||\
      defined(FLRL_RL_STAGE) || defined(FLRL_RL_WPS) || defined(FLRL_RD_NARROW_MEAN) || defined(FLRL_RL_RO_MAXB) ||          \
      defined(FLRL_RD_UNROLL) || defined(FLRL_HOST_WORKERS) || defined(FLRL_HOST_CHUNK) ||                \
@@ -70,6 +70,11 @@
 #endif
 #ifndef FLRL_RL_STAGE
 #define FLRL_RL_STAGE 15360  // LDS run staging per workgroup (bytes)
+#endif
+
+// RL encode: sub-chunks in flight per wave during the scan (register sets)
+#ifndef FLRL_RL_PF
+#define FLRL_RL_PF 1
 #endif
 
 // RL encode: minimum waves per SIMD the kernels are compiled for (5: five
