@@ -566,6 +566,11 @@ struct RlWave {
     {
         const uint32_t j0 = c0 == 0 ? 0u : 255u - c0;
         const bool split = with_split && j0 < L.fpos && j0 < L.vbl;
+        if constexpr (CH == 4) {  // one u64: the natural heads and the split bit
+            h0 = (((uint64_t)L.nat[1] << 32) | L.nat[0]) | (split ? 1ull << j0 : 0ull);
+            h1 = 0;
+            return;
+        }
         h0 = h1 = 0;
 #pragma unroll
         for (int c = 0; c < CH; ++c) {
@@ -584,7 +589,10 @@ struct RlWave {
     // value = the byte before h), records at slot, slot + 1, ...
     __device__ void lane_runs(const Sub &L, uint64_t h0, uint64_t h1, uint32_t c_first, uint32_t slot) const
     {
-        int prev = -1;
+        // before the lane's first head prev = -c_first: c_first + pos <= 255
+        // (a longer chunk would have a split head first), so every count is
+        // pos - prev with no modulo and no first-head branch in the loop
+        int prev = -(int)c_first;
         uint32_t val = L.p0;
         while (h0 | h1) {
             int pos;
@@ -595,7 +603,7 @@ struct RlWave {
                 pos = 64 + __builtin_ctzll(h1);
                 h1 &= h1 - 1;
             }
-            uint32_t cnt = prev < 0 ? add_c(c_first, (uint32_t)pos) : (uint32_t)(pos - prev);
+            uint32_t cnt = (uint32_t)(pos - prev);
             cnt = cnt == 0 ? 255u : cnt;
             const uint32_t q = (uint32_t)pos;
             const uint32_t nval = my[(((q >> 4) ^ sw) * 16) + (q & 15u)];
@@ -994,7 +1002,11 @@ __global__ __launch_bounds__(T, kRlWavesPerSimd) void rl_encode_wave_kernel(  //
     __shared__ uint64_t s_st[W];
 
     const int tid = threadIdx.x;
-    const int w = tid / kWave;
+    // the wave index in a scalar register: every chunk offset, length and
+    // "whole sub-chunk" test below is then wave-uniform, so the compiler emits
+    // scalar branches instead of executing masked tail paths (which it did,
+    // at ~40 VALU instructions per sub-chunk)
+    const int w = __builtin_amdgcn_readfirstlane(tid / kWave);
     const Wv V(in, n, s_lds, w);
     const uint32_t tile = blockIdx.x;  // (lookback_seg: why not a ticket)
     if (tile >= ntiles)
