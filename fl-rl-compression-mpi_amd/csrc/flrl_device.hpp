@@ -125,6 +125,11 @@ __device__ __forceinline__ uint64_t wave_shr1_64(uint64_t v)
 
 // Inclusive wave scan in six DPP steps (no LDS crossbar round trips):
 // row_shr 1/2/4/8 scan each row, row_bcast:15 and :31 carry row totals up.
+// Each step folds into one v_add_u32_dpp -- unless a caller's arithmetic on
+// the result (e.g. incl - own) lets the compiler reuse the shifted partial
+// sums, which then stay separate v_mov_b32_dpp + v_add pairs with wait
+// states between them (seen in the RL encode's scan loop): the empty asm
+// makes the result opaque, so the six steps stay six instructions.
 __device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t v)
 {
     v += dpp_up0<0x111, 0xF>(v);
@@ -133,6 +138,7 @@ __device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t v)
     v += dpp_up0<0x118, 0xF>(v);
     v += dpp_up0<0x142, 0xA>(v);
     v += dpp_up0<0x143, 0xC>(v);
+    asm volatile("" : "+v"(v));
     return v;
 }
 

@@ -343,6 +343,9 @@ __global__ __launch_bounds__(T + kWave, 1) void fl_encode_kernel(
 constexpr int kDecTilesPerRound = kDecThreads * 16 / kDecTileFrames;  // 16: a half-wave per tile
 constexpr int kDecBlockRounds = 4;                                    // tiles per block <= 64
 constexpr uint64_t kBaseTag = 1ull << 63;
+// block status words one per 128-byte line: every workgroup reads every
+// predecessor's word, and 16 words per line queued those reads on few lines
+constexpr int kDecStatusStride = FLRL_FL_DEC_STATUS_STRIDE;
 static_assert(kDecTileFrames == 32 * 16, "a tile's widths are one half-wave of 16-frame lanes");
 
 // Clamped widths of the 16 frames at f (f % 16 == 0; frames at or past nframes
@@ -395,14 +398,14 @@ __device__ __forceinline__ uint64_t fl_block_prefix(uint64_t *status, uint32_t b
 {
     const int tid = threadIdx.x;
     if (tid == 0)
-        granule_store(&status[blk], kFlagA | agg);
+        granule_store(&status[(size_t)blk * kDecStatusStride], kFlagA | agg);
     uint64_t sum = 0;
     for (uint32_t j0 = 0; j0 < blk; j0 += 4 * T) {
         uint64_t g[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const uint32_t j = j0 + (uint32_t)tid + (uint32_t)k * T;
-            g[k] = j < blk ? granule_load(&status[j]) : kFlagA;
+            g[k] = j < blk ? granule_load(&status[(size_t)j * kDecStatusStride]) : kFlagA;
         }
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
@@ -428,7 +431,7 @@ __device__ __forceinline__ uint64_t fl_block_prefix(uint64_t *status, uint32_t b
                     break;
                 }
                 __builtin_amdgcn_s_sleep(1);
-                g[k] = granule_load(&status[j]);
+                g[k] = granule_load(&status[(size_t)j * kDecStatusStride]);
             }
             sum += g[k] & kPayload;
         }
@@ -705,7 +708,7 @@ __global__ __launch_bounds__(kDecThreads, kDecPerCU) void fl_decode_kernel(
 
 // ---- scratch layout ---------------------------------------------------------
 // [Ctrl 16 B][encode: status lines[enc_tiles]]   or
-// [Ctrl 16 B][decode: status[dec_blocks] (16-B padded)][tile_base[dec_tiles + 1]]
+// [Ctrl 16 B][decode: status lines[dec_blocks]][tile_base[dec_tiles + 1]]
 // all zeroed per call (the decode's tile_base holds tagged granules). Offsets
 // blocks of dec_tb tiles: one per decode workgroup (2 per CU x 256 CUs) up to
 // 2 GiB, 64 tiles (4 MiB of output) each past that.
@@ -722,7 +725,7 @@ struct FlLayout {
                                        ? (size_t)kDecTilesPerRound * kDecBlockRounds : dec_tb);
         dec_blocks = div_up(dec_tiles, dec_tb);
         enc_zero = FLRL_FL_STATUS_OFF + round_up(enc_tiles * 8 * FLRL_FL_STATUS_STRIDE, 16);
-        dec_zero = sizeof(Ctrl) + round_up(dec_blocks * 8, 16) + round_up((dec_tiles + 1) * 8, 16);
+        dec_zero = sizeof(Ctrl) + dec_blocks * 8 * kDecStatusStride + round_up((dec_tiles + 1) * 8, 16);
         bytes = enc_zero > dec_zero ? enc_zero : dec_zero;
     }
 };
@@ -803,7 +806,7 @@ extern "C" int flrl_fl_decode_device(const uint8_t *d_bits, size_t bits_size,
     Ctrl *ctrl = static_cast<Ctrl *>(d_scratch);
     uint64_t *status = reinterpret_cast<uint64_t *>(ctrl + 1);
     uint64_t *tile_base = reinterpret_cast<uint64_t *>(static_cast<uint8_t *>(d_scratch) + sizeof(Ctrl) +
-                                                       round_up(L.dec_blocks * 8, 16));
+                                                       L.dec_blocks * 8 * kDecStatusStride);
     const size_t dgrid = (size_t)kDecPerCU * (size_t)cu_count();
     kernel_timing_begin(s);
     hipLaunchKernelGGL(fl_decode_kernel<kDecItems>,

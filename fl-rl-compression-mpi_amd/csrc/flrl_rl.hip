@@ -86,9 +86,18 @@ __device__ __forceinline__ uint32_t pm_compose(uint32_t a, uint32_t b)
 {
     return (b & kMapConst) ? b : a + b;
 }
+// x mod 255 without the quarter-rate multiplies of a division: 256 = 1 (mod
+// 255), so x's byte sum (one dot product, <= 1020) keeps its residue; a second
+// fold leaves <= 258 and one subtract finishes
+__device__ __forceinline__ uint32_t mod255(uint32_t x)
+{
+    uint32_t s = __builtin_amdgcn_udot4(x, 0x01010101u, 0u, false);
+    s = (s & 0xFFu) + (s >> 8);
+    return s >= 255u ? s - 255u : s;
+}
 __device__ __forceinline__ uint32_t pm_apply(uint32_t m, uint32_t c)
 {
-    return ((m & kMapConst) ? (m & ~kMapConst) : c + m) % 255u;
+    return mod255((m & kMapConst) ? (m & ~kMapConst) : c + m);
 }
 // inclusive PhaseMap scan, DPP steps as wave_incl_scan_u32 (0 = identity map)
 __device__ __forceinline__ uint32_t wave_incl_scan_map(uint32_t m)
@@ -591,9 +600,13 @@ struct RlWave {
     {
         // before the lane's first head prev = -c_first: c_first + pos <= 255
         // (a longer chunk would have a split head first), so every count is
-        // pos - prev with no modulo and no first-head branch in the loop
-        int prev = -(int)c_first;
+        // pos - prev in [1, 255] with no modulo and no branch in the loop; the
+        // state 0 stands for 255 bytes (a head at pos 0 then ends a 255-run).
+        // (The chunk's first natural head gets a count here that emit()
+        // replaces: it depends on the tile's incoming state.)
+        int prev = c_first == 0 ? -255 : -(int)c_first;
         uint32_t val = L.p0;
+        const uint32_t sw16 = sw << 4;  // image byte of lane position q: (((q >> 4) ^ sw) << 4) | (q & 15)
         while (h0 | h1) {
             int pos;
             if (h0) {
@@ -603,10 +616,8 @@ struct RlWave {
                 pos = 64 + __builtin_ctzll(h1);
                 h1 &= h1 - 1;
             }
-            uint32_t cnt = (uint32_t)(pos - prev);
-            cnt = cnt == 0 ? 255u : cnt;
-            const uint32_t q = (uint32_t)pos;
-            const uint32_t nval = my[(((q >> 4) ^ sw) * 16) + (q & 15u)];
+            const uint32_t cnt = (uint32_t)(pos - prev);
+            const uint32_t nval = my[(uint32_t)pos ^ sw16];
             stc[slot] = (uint8_t)cnt;
             stv[slot] = (uint8_t)val;
             val = nval;

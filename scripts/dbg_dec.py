@@ -23,7 +23,7 @@ for n in [int(a) for a in sys.argv[1:]]:
     ntiles = -(-n // 65536)
     tb = max(1, min(64, -(-ntiles // 512)))
     nb = -(-ntiles // tb)
-    off = 16 + ((nb * 8 + 15) // 16) * 16
+    off = 16 + nb * 128
     raw = d.scratch[off:off + 8 * (ntiles + 1)].cpu().numpy().view(np.uint64)
     w = np.clip(d.bits[:d.frames].cpu().numpy().astype(np.int64), 1, 8)
     ref = np.concatenate([[0], np.cumsum([w[t * 512:(t + 1) * 512].sum() for t in range(ntiles)])])
