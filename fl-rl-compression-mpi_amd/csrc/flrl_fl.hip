@@ -507,6 +507,13 @@ __device__ __forceinline__ void fl_decode_offsets(const uint8_t *__restrict__ bi
     }
     if (t1 == ntiles && tid == 0)
         granule_store(&tile_base[ntiles], kBaseTag | (base + run));
+    // the block is complete (P) once every storing wave's stores are done: a
+    // reader that sees P finds every entry tagged (granules: each entry is
+    // also readable on its own by its tag)
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    if (tid == 0)
+        granule_store(&status[(size_t)blk * kDecStatusStride], kFlagP | run);
     if (has_last) {
         const uint32_t b_last = clamp_width(bits[nframes - 1]);
         const uint64_t cnt = n - (nframes - 1) * kFrame;
@@ -516,12 +523,72 @@ __device__ __forceinline__ void fl_decode_offsets(const uint8_t *__restrict__ bi
     }
 }
 
-// Tile t's offset and 16-byte units from the tagged tile_base entries (spins
-// while phase 1 has not written them; every thread of the workgroup, uniform).
-__device__ __forceinline__ bool tile_span(uint64_t *tile_base, uint32_t t, uint64_t &base, uint32_t &agg,
+// Phase 1's inputs, for tile_span's fallback.
+struct DecOffsets {
+    const uint8_t *bits;
+    uint64_t nframes, vsize, n;
+    uint64_t *tile_base, *status;
+    uint32_t ntiles, TB;
+    uint64_t help_ticks;
+    uint32_t *s_wave2;
+    uint64_t *s_red;
+};
+
+// Phase 1 complete: every block's status word reads P (written after the
+// block's tagged offsets, fl_decode_offsets), so the decode loop never waits
+// on an offset. A block's owner (workgroup index = block) can be a workgroup
+// that has not started -- other kernels on the GPU holding the CUs while this
+// launch's resident workgroups wait (the 4-stream test did this) -- so past
+// help_ticks the waiting workgroup computes a missing block itself (the same
+// values the owner writes). Kept out of the decode loop: inlined there, the
+// fallback's registers cost the loop its second workgroup per CU.
+__device__ __forceinline__ void dec_wait_blocks(const DecOffsets &P, uint32_t nblocks, Ctrl *ctrl,
+                                                uint32_t *s_min)
+{
+    const int tid = threadIdx.x;
+    uint64_t t0 = 0;
+    uint32_t spins = 0;
+    for (;;) {
+        uint32_t miss = 0xFFFFFFFFu;
+        for (uint32_t b = tid; b < nblocks; b += kDecThreads)
+            if ((granule_load(&P.status[(size_t)b * kDecStatusStride]) >> 62) != 2 && miss == 0xFFFFFFFFu)
+                miss = b;
+        if (!__syncthreads_or(miss != 0xFFFFFFFFu))
+            return;
+        const uint64_t now = __builtin_amdgcn_s_memrealtime();
+        if (t0 == 0)
+            t0 = now;
+        // the clock is per wave: the decision must be the workgroup's (the
+        // help path has barriers), so it goes through one
+        if (__syncthreads_or(now - t0 >= P.help_ticks)) {
+            if (tid == 0)
+                *s_min = 0xFFFFFFFFu;
+            __syncthreads();
+            if (miss != 0xFFFFFFFFu)
+                atomicMin(s_min, miss);
+            __syncthreads();
+            const uint32_t b = *s_min;
+            if (b < nblocks)
+                fl_decode_offsets<kDecThreads>(P.bits, P.nframes, P.vsize, P.n, P.tile_base, P.ntiles, b, P.TB,
+                                               P.status, P.help_ticks, ctrl, P.s_wave2, P.s_red);
+            t0 = 0;
+            continue;
+        }
+        if (++spins > kSpinLimit) {
+            if (tid == 0)
+                raise_error(ctrl, FLRL_E_TIMEOUT);
+            return;
+        }
+        __builtin_amdgcn_s_sleep(2);
+    }
+}
+
+// Tile t's offset and 16-byte units from its tagged tile_base entries (every
+// thread of the workgroup, uniform; after dec_wait_blocks they are all set).
+__device__ __forceinline__ bool tile_span(const DecOffsets &P, uint32_t t, uint64_t &base, uint32_t &agg,
                                           Ctrl *ctrl)
 {
-    uint64_t a = granule_load(&tile_base[t]), e = granule_load(&tile_base[t + 1]);
+    uint64_t a = granule_load(&P.tile_base[t]), e = granule_load(&P.tile_base[t + 1]);
     uint32_t spins = 0;
     while (!(a & e & kBaseTag)) {
         if (++spins > kSpinLimit) {
@@ -530,8 +597,8 @@ __device__ __forceinline__ bool tile_span(uint64_t *tile_base, uint32_t t, uint6
             return false;
         }
         __builtin_amdgcn_s_sleep(2);
-        a = granule_load(&tile_base[t]);
-        e = granule_load(&tile_base[t + 1]);
+        a = granule_load(&P.tile_base[t]);
+        e = granule_load(&P.tile_base[t + 1]);
     }
     base = a & ~kBaseTag;
     agg = (uint32_t)((e & ~kBaseTag) - base);
@@ -605,6 +672,9 @@ __global__ __launch_bounds__(kDecThreads, kDecPerCU) void fl_decode_kernel(
     for (uint32_t blk = blockIdx.x; blk < nblocks; blk += gridDim.x)
         fl_decode_offsets<T>(bits, nframes, vsize, n, tile_base, ntiles, blk, TB, status, help_ticks, ctrl,
                              s_wave2, s_red);
+    const DecOffsets P{bits, nframes, vsize, n, tile_base, status, ntiles, TB, help_ticks, s_wave2, s_red};
+    if (blockIdx.x < ntiles)
+        dec_wait_blocks(P, nblocks, ctrl, &s_next[0]);
 
     // ---- phase 2: decode. The first two tiles are grid-stride (no atomic
     // round trip at the launch, when every workgroup would queue on the counter
@@ -616,7 +686,7 @@ __global__ __launch_bounds__(kDecThreads, kDecPerCU) void fl_decode_kernel(
     uint32_t slot = 1;
     uint64_t base = 0;
     uint32_t agg = 0;
-    if (tile < ntiles && tile_span(tile_base, tile, base, agg, ctrl)) {
+    if (tile < ntiles && tile_span(P, tile, base, agg, ctrl)) {
         u32x4 a[ITEMS];
         dec_load_values<ITEMS>(a, values, base, agg, vsize);
         uint64_t wv = dec_load_widths(bits, (uint64_t)tile * TF + (tid >> 3) * ITEMS, nframes);
@@ -655,7 +725,7 @@ __global__ __launch_bounds__(kDecThreads, kDecPerCU) void fl_decode_kernel(
             bool more = nxt < ntiles;
             const uint64_t tile_off = (uint64_t)tile * TB_BYTES;
             if (more) {
-                more = tile_span(tile_base, nxt, base, agg, ctrl);
+                more = tile_span(P, nxt, base, agg, ctrl);
                 if (more) {
                     dec_load_values<ITEMS>(a, values, base, agg, vsize);
                     wv = dec_load_widths(bits, (uint64_t)nxt * TF + (tid >> 3) * ITEMS, nframes);

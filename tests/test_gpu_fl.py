@@ -485,3 +485,29 @@ def test_concurrent_streams():
             assert rl[i].error() == 0 and rl[i].runs() == R, (rep, i)
             assert torch.equal(rl[i].counts[:R], c0) and torch.equal(rl[i].values[:R], rv0), (rep, i)
             assert torch.equal(rl[i].out[: sizes[2 + i]], xs[2 + i][: sizes[2 + i]]), (rep, i)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [(48 << 20) + 5, 1 << 30, 100_003])
+def test_decode_offsets_fallback_bit_exact(n):
+    """The FL decode computes its tile offsets in-kernel (phase 1, one block of
+    tiles per workgroup); a block whose owner has not started is computed by
+    a waiting workgroup after a timeout (the decoupled fallback: other kernels
+    can hold the CUs). flrl_debug_lookback_help_us(0) takes the fallback at
+    every wait: the decode must stay bit-exact and error-free."""
+    import flrl
+    from flrl.device import FLDevice, gen
+    x = gen("lo4", n, 5)
+    x[n // 3] = 0xFF
+    d = FLDevice(n)
+    d.encode(x)
+    v = d.values_size()
+    flrl.debug_lookback_help_us(0)
+    try:
+        for _ in range(3):
+            out = d.decode(v)
+            torch.cuda.synchronize()
+            assert d.error() == 0
+            assert torch.equal(out, x[:n])
+    finally:
+        flrl.debug_lookback_help_us(-1)
