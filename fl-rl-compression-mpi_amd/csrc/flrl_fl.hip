@@ -22,13 +22,13 @@
 // were chosen by measurement (scripts/ubench_encode.hip, scripts/ab_encode.py,
 // DESIGN.md §Encode).
 //
-// Decode is ONE launch of fl_decode_kernel: each workgroup first computes the
-// output offsets of its block of tiles (frame widths summed, validated; block
-// bases by an all-predecessor prefix) and stores them as tagged granules, then
-// takes 64 KiB output tiles (the first two grid-stride, then by ticket), loads
-// each tile's widths and contiguous packed bytes (16-B aligned) one tile ahead
-// into registers, stages the bytes in LDS and unpacks 2b bytes -> 16 bytes per
-// lane. A tile's offsets are polled by their tag, so the two phases overlap.
+// Decode is two launches: fl_offsets_kernel scans the frame widths (F bytes,
+// <1% of the traffic) into per-tile output offsets and validates the widths
+// and valuesSize; fl_decode_kernel is then a streaming kernel with no
+// inter-workgroup dependency: persistent grid-stride workgroups take 32 KiB
+// output tiles, load each tile's widths and contiguous packed bytes (16-B
+// aligned) one tile ahead into registers, stage the bytes in LDS and unpack
+// 2b bytes -> 16 bytes per lane.
 //
 // Replaces the reference kernels compressCalculateOutputBits
 // (fl_gpu.cu:648-685), compressInitializeFrameStartIndiciesBits + thrust scan
@@ -57,7 +57,13 @@ constexpr int kDecItems = 8;      // decode tile = 512 lanes x 8 x 16 B = 64 KiB
 constexpr int kDecPerCU = 2;      // persistent decode workgroups per CU (LDS 64 KiB each)
 constexpr int kDecTileBytes = kDecThreads * 16 * kDecItems;
 constexpr int kDecTileFrames = kDecTileBytes / kFrame;
-constexpr uint64_t kFlHelpTicks = 20000;  // decode phase 1: a predecessor block unpublished 200 us is computed
+constexpr int kOffStatusStride = FLRL_FL_OFF_STATUS_STRIDE;  // pre-pass status granules per block (one line)
+constexpr uint64_t kFlHelpTicks = 20000;  // pre-pass: a predecessor unpublished for 200 us is computed
+constexpr int kOffFramesPerThread = 128;  // (64: 1 GiB decode call +1 %, more workgroups to scan; 256: equal)
+constexpr int kOffFrames = kThreads * kOffFramesPerThread;  // frames per offsets workgroup
+constexpr int kOffLanesPerTile = kDecTileFrames / kOffFramesPerThread;  // offsets lanes per decode tile
+static_assert(kOffLanesPerTile * kOffFramesPerThread == kDecTileFrames && kThreads % kOffLanesPerTile == 0,
+              "a decode tile is whole offsets lanes");
 
 // Pack 8 bytes (each < 2^b) of x into the low 8b bits, value i at bit b*i.
 __device__ __forceinline__ uint64_t pack8(uint64_t x, uint32_t b)
@@ -328,281 +334,143 @@ __global__ __launch_bounds__(T + kWave, 1) void fl_encode_kernel(
     }
 }
 
-// ---- FL decode, phase 1: the tile offsets inside the decode launch ---------
-// (Until round 3 a separate pre-pass kernel, fl_offsets_kernel, wrote them:
-// with its zero-fill and the launch boundary it cost ~20 us of a 1 GiB decode
-// call) Workgroup w first computes the output offset
-// (16-byte units) of every tile of offsets block w: kDecBlockRounds rounds of
-// 16 tiles at most (each lane sums the widths of 16 frames, SWAR-validated and
-// clamped as the decode clamps them; a half-wave is one tile), the block's
-// base from every predecessor block's aggregate (fl_block_prefix, one round
-// trip once they are published), and stores each tile's absolute offset as a
-// TAGGED granule (kBaseTag): the decode loop polls the tag, so no grid-wide
-// barrier separates the phases and an entry is never read before it is
-// written. The scratch (status words and tile_base) is zeroed per call.
-constexpr int kDecTilesPerRound = kDecThreads * 16 / kDecTileFrames;  // 16: a half-wave per tile
-constexpr int kDecBlockRounds = 4;                                    // tiles per block <= 64
-constexpr uint64_t kBaseTag = 1ull << 63;
-// block status words one per 128-byte line: every workgroup reads every
-// predecessor's word, and 16 words per line queued those reads on few lines
-constexpr int kDecStatusStride = FLRL_FL_DEC_STATUS_STRIDE;
-static_assert(kDecTileFrames == 32 * 16, "a tile's widths are one half-wave of 16-frame lanes");
-
 // Clamped widths of the 16 frames at f (f % 16 == 0; frames at or past nframes
-// count 0); bad: a width outside [1, 8] (FLRL_E_FORMAT, clamped like the decode).
-__device__ __forceinline__ uint32_t sum16_widths(const uint8_t *bits, uint64_t f, uint64_t nframes, bool &bad)
+// count 0): the decoupled fallback's sum of a predecessor block.
+__device__ __forceinline__ uint64_t sum_widths(const uint8_t *bits, uint64_t fa, uint64_t fb)
 {
-    if (f >= nframes)
-        return 0;
-    uint32_t sum = 0;
-    if (f + 16 <= nframes) {
-        const u32x4 q = *reinterpret_cast<const u32x4 *>(bits + f);
-#pragma unroll
-        for (int d = 0; d < 4; ++d) {
-            const uint32_t x = q[d];
-            const uint32_t zero = (x - 0x01010101u) & ~x & 0x80808080u;
-            const uint32_t big = (((x & 0x7F7F7F7Fu) + 0x77777777u) | x) & 0x80808080u;
-            if (zero | big) {  // rare: clamp byte by byte
-                bad = true;
-                for (int i = 0; i < 4; ++i)
-                    sum += clamp_width((x >> (8 * i)) & 0xFFu);
-            } else {
-                const uint32_t h = (x & 0x00FF00FFu) + ((x >> 8) & 0x00FF00FFu);
-                sum += (h & 0xFFFFu) + (h >> 16);
-            }
-        }
-    } else {
-        const u32x4 q = load16_tail(bits, f, nframes);
-        for (int i = 0; i < 16 && f + i < nframes; ++i) {
-            const uint32_t raw = (q[i >> 2] >> (8 * (i & 3))) & 0xFFu;
-            bad |= raw < 1 || raw > 8;
-            sum += clamp_width(raw);
-        }
+    uint64_t h = 0;
+    for (uint64_t f = fa; f < fb; f += 16) {
+        const u32x4 q = load16_tail(bits, f, fb);
+        for (int i = 0; i < 16 && f + i < fb; ++i)
+            h += clamp_width((q[i >> 2] >> (8 * (i & 3))) & 0xFFu);
     }
-    return sum;
+    return h;
 }
 
-// Exclusive prefix of the blocks' aggregates (block_prefix_all with a
-// decoupled fallback): the workgroup publishes its aggregate, then every
-// thread loads its share of ALL predecessors' words at once. Blocks are
-// numbered by workgroup index (a ticket per launch start would queue 512
-// workgroups on one counter); the dispatcher starts them in index order on
-// each XCD, so an unpublished predecessor is running or about to start -- but
-// with other look-back kernels on the GPU it may not start for a long time, so
-// a word still unpublished after help_ticks (s_memrealtime) is computed by the
-// waiting lane from the widths instead (the block's frames [j TB F, ...)).
-template <int T>
-__device__ __forceinline__ uint64_t fl_block_prefix(uint64_t *status, uint32_t blk, uint64_t agg,
-                                                    const uint8_t *bits, uint64_t nframes, uint64_t block_frames,
-                                                    uint64_t help_ticks, Ctrl *ctrl, uint64_t *s_red)
+// Decode pre-pass: one workgroup scans `iters` x kOffFrames frame widths (64
+// per lane per round), validates them (a width outside [1,8] raises
+// FLRL_E_FORMAT and is clamped, as fl_decode_kernel clamps it, so offsets stay
+// consistent and in bounds), and writes the output offset (16-byte units) of
+// each 256-frame decode tile: tile_base[t] for t < ntiles and tile_base[ntiles]
+// = total. Offsets are first written workgroup-relative; once the workgroup's
+// base is known (block_prefix_all_help: iters keeps the grid within
+// kMaxPrefixBlocks) each lane adds it to the entries it wrote. The workgroup
+// holding the last frame checks valuesSize against the widths. Blocks are
+// numbered by workgroup index (a ticket per workgroup queued the whole launch
+// on one counter at its start), with the decoupled fallback of
+// block_prefix_all_help; a launch counts exactly nblocks arrivals on the reset
+// counter (Ctrl::aux), more means its scratch was not reset.
+__global__ __launch_bounds__(kThreads) void fl_offsets_kernel(
+    const uint8_t *__restrict__ bits, uint64_t nframes, uint64_t vsize, uint64_t n,
+    uint64_t *__restrict__ tile_base, uint32_t ntiles, uint32_t nblocks, uint32_t iters, Ctrl *ctrl,
+    uint64_t *status, uint64_t help_ticks)
 {
-    const int tid = threadIdx.x;
-    if (tid == 0)
-        granule_store(&status[(size_t)blk * kDecStatusStride], kFlagA | agg);
-    uint64_t sum = 0;
-    for (uint32_t j0 = 0; j0 < blk; j0 += 4 * T) {
-        uint64_t g[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const uint32_t j = j0 + (uint32_t)tid + (uint32_t)k * T;
-            g[k] = j < blk ? granule_load(&status[(size_t)j * kDecStatusStride]) : kFlagA;
-        }
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const uint32_t j = j0 + (uint32_t)tid + (uint32_t)k * T;
-            uint64_t t0 = 0;
-            uint32_t spins = 0;
-            while ((g[k] >> 62) == 0) {
-                const uint64_t now = __builtin_amdgcn_s_memrealtime();
-                if (t0 == 0)
-                    t0 = now;
-                if (now - t0 >= help_ticks) {  // block j's aggregate from its widths
-                    bool bad = false;
-                    uint64_t h = 0;
-                    const uint64_t fa = (uint64_t)j * block_frames;
-                    const uint64_t fb = fa + block_frames < nframes ? fa + block_frames : nframes;
-                    for (uint64_t f = fa; f < fb; f += 16)
-                        h += sum16_widths(bits, f, fb, bad);
-                    g[k] = kFlagA | h;
-                    break;
-                }
-                if (++spins > kSpinLimit) {
-                    raise_error(ctrl, FLRL_E_TIMEOUT);
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(1);
-                g[k] = granule_load(&status[(size_t)j * kDecStatusStride]);
-            }
-            sum += g[k] & kPayload;
-        }
-    }
-    sum = wave_sum_u64(sum);
-    if ((tid & (kWave - 1)) == 0)
-        s_red[tid / kWave] = sum;
-    __syncthreads();
-    uint64_t excl = 0;
-#pragma unroll
-    for (int v = 0; v < T / kWave; ++v)
-        excl += s_red[v];
-    return excl;
-}
-
-// Phase 1 for offsets block `blk` (tiles [blk TB, (blk+1) TB) of ntiles):
-// tile_base[t] = kBaseTag | offset of tile t; the last block also writes
-// tile_base[ntiles] = kBaseTag | total and checks valuesSize against the widths.
-template <int T>
-__device__ __forceinline__ void fl_decode_offsets(const uint8_t *__restrict__ bits, uint64_t nframes,
-                                                  uint64_t vsize, uint64_t n, uint64_t *tile_base,
-                                                  uint32_t ntiles, uint32_t blk, uint32_t TB, uint64_t *status,
-                                                  uint64_t help_ticks, Ctrl *ctrl, uint32_t *s_wave2,
-                                                  uint64_t *s_red)
-{
+    __shared__ uint32_t s_wave[kWaves];
+    __shared__ uint64_t s_red[kWaves];
     const int tid = threadIdx.x;
     const int lane = tid & (kWave - 1);
     const int wave = tid / kWave;
-    constexpr int W = T / kWave;
-    const uint32_t t0 = blk * TB;
-    const uint32_t t1 = t0 + TB < ntiles ? t0 + TB : ntiles;
-    const uint64_t f_end = (uint64_t)t1 * kDecTileFrames < nframes ? (uint64_t)t1 * kDecTileFrames : nframes;
-    const uint32_t rounds = (t1 - t0 + kDecTilesPerRound - 1) / kDecTilesPerRound;
-    uint64_t run = 0;  // block-relative units before this round
-    uint32_t rel[kDecBlockRounds];  // this half-wave's tile offset, block-relative (lanes 0 and 32)
-    bool bad = false, has_last = false;
-    uint64_t last_units = 0;  // block-relative units before the last frame (its lane)
-    for (uint32_t r = 0; r < rounds; ++r) {
-        const uint64_t f = ((uint64_t)t0 + r * kDecTilesPerRound) * kDecTileFrames + (uint64_t)tid * 16;
-        const uint32_t sum = f < f_end ? sum16_widths(bits, f, f_end, bad) : 0u;
-        const uint32_t inc = wave_incl_scan_u32(sum);
-        const uint32_t h0 = (uint32_t)__builtin_amdgcn_readlane((int)inc, 31);  // first half-wave's tile
-        uint32_t *sw = s_wave2 + (r & 1) * W;  // alternating: rewritten two barriers after its read
-        if (lane == kWave - 1)
-            sw[wave] = inc;
-        __syncthreads();
-        uint32_t before = 0, tot = 0;
+    const uint32_t blk = blockIdx.x;
+    uint64_t local = 0;          // frames' 16-byte units before this round, workgroup-relative
+    bool has_last = false;       // this lane holds the last frame
+    uint64_t last_local = 0;     // its units before the last frame, workgroup-relative
+    bool bad = false;
+    uint64_t keep = 0;
+    for (uint32_t it = 0; it < iters; ++it) {
+        const uint64_t f0 = ((uint64_t)blk * iters + it) * kOffFrames + (uint64_t)tid * kOffFramesPerThread;
+        // all of the lane's width loads in flight before any is used
+        constexpr int Q = kOffFramesPerThread / 16;
+        u32x4 wq[Q];
+        if (f0 + kOffFramesPerThread <= nframes) {
 #pragma unroll
-        for (int v = 0; v < W; ++v) {
-            const uint32_t x = sw[v];
-            before += v < wave ? x : 0u;
-            tot += x;
+            for (int q = 0; q < Q; ++q)
+                wq[q] = *reinterpret_cast<const u32x4 *>(bits + f0 + 16 * q);
+        } else {
+#pragma unroll
+            for (int q = 0; q < Q; ++q)
+                wq[q] = load16_tail(bits, f0 + 16 * q, nframes);
         }
-        rel[r & (kDecBlockRounds - 1)] = (uint32_t)run + before + (lane >= 32 ? h0 : 0u);
-        if (f < f_end && nframes <= f + 16) {  // this lane (of this block) holds the last frame
+        // widths 4 per dword (SWAR): a byte is invalid if it is 0 or > 8
+        uint32_t sum = 0;
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            const uint64_t fq = f0 + 16 * q;
+            if (fq + 16 <= nframes) {
+#pragma unroll
+                for (int d = 0; d < 4; ++d) {
+                    const uint32_t x = wq[q][d];
+                    const uint32_t zero = (x - 0x01010101u) & ~x & 0x80808080u;
+                    const uint32_t big = (((x & 0x7F7F7F7Fu) + 0x77777777u) | x) & 0x80808080u;
+                    if (zero | big) {  // rare: clamp byte by byte
+                        bad = true;
+                        for (int i = 0; i < 4; ++i)
+                            sum += clamp_width((x >> (8 * i)) & 0xFFu);
+                    } else {
+                        const uint32_t h = (x & 0x00FF00FFu) + ((x >> 8) & 0x00FF00FFu);
+                        sum += (h & 0xFFFFu) + (h >> 16);
+                    }
+                }
+            } else {
+                for (int i = 0; i < 16 && fq + i < nframes; ++i) {
+                    const uint32_t raw = (wq[q][i >> 2] >> (8 * (i & 3))) & 0xFFu;
+                    bad |= raw < 1 || raw > 8;
+                    sum += clamp_width(raw);
+                }
+            }
+        }
+        // exclusive scan of lane sums over the workgroup
+        const uint32_t inc = wave_incl_scan_u32(sum);
+        if (it > 0)
+            __syncthreads();  // the previous round's s_wave readers are done
+        if (lane == kWave - 1)
+            s_wave[wave] = inc;
+        __syncthreads();
+        uint32_t before = 0, agg = 0;
+#pragma unroll
+        for (int w = 0; w < kWaves; ++w) {
+            before += w < wave ? s_wave[w] : 0u;
+            agg += s_wave[w];
+        }
+        const uint32_t excl = before + inc - sum;
+        const uint64_t tile = f0 / kDecTileFrames;
+        if (tid % kOffLanesPerTile == 0 && tile < ntiles) {
+            if (iters == 1)
+                keep = local + excl;  // one round: the entry waits in a register for the base
+            else
+                tile_base[tile] = local + excl;
+        }
+        if (nframes > f0 && nframes <= f0 + kOffFramesPerThread) {
             has_last = true;
-            // the last frame is this lane's last: its units before it are the
-            // lane's exclusive prefix plus its own sum less the last width
-            last_units = run + before + inc - clamp_width(bits[nframes - 1]);
+            last_local = local + excl + sum - clamp_width(bits[nframes - 1]);
         }
-        run += tot;
+        local += agg;
     }
     if (bad)
         raise_error(ctrl, FLRL_E_FORMAT);
-    const uint64_t base = fl_block_prefix<T>(status, blk, run, bits, nframes, (uint64_t)TB * kDecTileFrames,
-                                             help_ticks, ctrl, s_red);
-    if ((lane & 31) == 0) {
-        for (uint32_t r = 0; r < rounds; ++r) {
-            const uint32_t t = t0 + r * kDecTilesPerRound + (uint32_t)(tid >> 5);
-            if (t < t1)
-                granule_store(&tile_base[t], kBaseTag | (base + rel[r & (kDecBlockRounds - 1)]));
-        }
+    const uint64_t block_frames = (uint64_t)iters * kOffFrames;
+    auto help = [&](uint32_t j) -> uint64_t {  // block j's aggregate from its widths
+        const uint64_t fa = (uint64_t)j * block_frames;
+        return sum_widths(bits, fa, fa + block_frames < nframes ? fa + block_frames : nframes);
+    };
+    const uint64_t base =
+        block_prefix_all_help<kThreads, kOffStatusStride>(status, blk, local, ctrl, s_red, help_ticks, help);
+    for (uint32_t it = 0; it < iters; ++it) {
+        const uint64_t f0 = ((uint64_t)blk * iters + it) * kOffFrames + (uint64_t)tid * kOffFramesPerThread;
+        const uint64_t tile = f0 / kDecTileFrames;
+        if (tid % kOffLanesPerTile == 0 && tile < ntiles)
+            tile_base[tile] = iters == 1 ? keep + base : tile_base[tile] + base;  // this lane's own entry
     }
-    if (t1 == ntiles && tid == 0)
-        granule_store(&tile_base[ntiles], kBaseTag | (base + run));
-    // the block is complete (P) once every storing wave's stores are done: a
-    // reader that sees P finds every entry tagged (granules: each entry is
-    // also readable on its own by its tag)
-    __builtin_amdgcn_s_waitcnt(0);
-    __syncthreads();
-    if (tid == 0)
-        granule_store(&status[(size_t)blk * kDecStatusStride], kFlagP | run);
+    if (blk + 1 == nblocks && tid == 0)
+        tile_base[ntiles] = base + local;
     if (has_last) {
         const uint32_t b_last = clamp_width(bits[nframes - 1]);
         const uint64_t cnt = n - (nframes - 1) * kFrame;
-        const uint64_t expect = 16ull * (base + last_units) + (cnt * b_last + 7) / 8;
+        const uint64_t expect = 16ull * (base + last_local) + (cnt * b_last + 7) / 8;
         if (expect != vsize)
             raise_error(ctrl, FLRL_E_FORMAT);
     }
-}
-
-// Phase 1's inputs, for tile_span's fallback.
-struct DecOffsets {
-    const uint8_t *bits;
-    uint64_t nframes, vsize, n;
-    uint64_t *tile_base, *status;
-    uint32_t ntiles, TB;
-    uint64_t help_ticks;
-    uint32_t *s_wave2;
-    uint64_t *s_red;
-};
-
-// Phase 1 complete: every block's status word reads P (written after the
-// block's tagged offsets, fl_decode_offsets), so the decode loop never waits
-// on an offset. A block's owner (workgroup index = block) can be a workgroup
-// that has not started -- other kernels on the GPU holding the CUs while this
-// launch's resident workgroups wait (the 4-stream test did this) -- so past
-// help_ticks the waiting workgroup computes a missing block itself (the same
-// values the owner writes). Kept out of the decode loop: inlined there, the
-// fallback's registers cost the loop its second workgroup per CU.
-__device__ __forceinline__ void dec_wait_blocks(const DecOffsets &P, uint32_t nblocks, Ctrl *ctrl,
-                                                uint32_t *s_min)
-{
-    const int tid = threadIdx.x;
-    uint64_t t0 = 0;
-    uint32_t spins = 0;
-    for (;;) {
-        uint32_t miss = 0xFFFFFFFFu;
-        for (uint32_t b = tid; b < nblocks; b += kDecThreads)
-            if ((granule_load(&P.status[(size_t)b * kDecStatusStride]) >> 62) != 2 && miss == 0xFFFFFFFFu)
-                miss = b;
-        if (!__syncthreads_or(miss != 0xFFFFFFFFu))
-            return;
-        const uint64_t now = __builtin_amdgcn_s_memrealtime();
-        if (t0 == 0)
-            t0 = now;
-        // the clock is per wave: the decision must be the workgroup's (the
-        // help path has barriers), so it goes through one
-        if (__syncthreads_or(now - t0 >= P.help_ticks)) {
-            if (tid == 0)
-                *s_min = 0xFFFFFFFFu;
-            __syncthreads();
-            if (miss != 0xFFFFFFFFu)
-                atomicMin(s_min, miss);
-            __syncthreads();
-            const uint32_t b = *s_min;
-            if (b < nblocks)
-                fl_decode_offsets<kDecThreads>(P.bits, P.nframes, P.vsize, P.n, P.tile_base, P.ntiles, b, P.TB,
-                                               P.status, P.help_ticks, ctrl, P.s_wave2, P.s_red);
-            t0 = 0;
-            continue;
-        }
-        if (++spins > kSpinLimit) {
-            if (tid == 0)
-                raise_error(ctrl, FLRL_E_TIMEOUT);
-            return;
-        }
-        __builtin_amdgcn_s_sleep(2);
-    }
-}
-
-// Tile t's offset and 16-byte units from its tagged tile_base entries (every
-// thread of the workgroup, uniform; after dec_wait_blocks they are all set).
-__device__ __forceinline__ bool tile_span(const DecOffsets &P, uint32_t t, uint64_t &base, uint32_t &agg,
-                                          Ctrl *ctrl)
-{
-    uint64_t a = granule_load(&P.tile_base[t]), e = granule_load(&P.tile_base[t + 1]);
-    uint32_t spins = 0;
-    while (!(a & e & kBaseTag)) {
-        if (++spins > kSpinLimit) {
-            if (threadIdx.x == 0)
-                raise_error(ctrl, FLRL_E_TIMEOUT);
-            return false;
-        }
-        __builtin_amdgcn_s_sleep(2);
-        a = granule_load(&P.tile_base[t]);
-        e = granule_load(&P.tile_base[t + 1]);
-    }
-    base = a & ~kBaseTag;
-    agg = (uint32_t)((e & ~kBaseTag) - base);
-    return true;
+    if (tid == 0 && atomicAdd(reinterpret_cast<uint32_t *>(&ctrl->aux), 1u) >= nblocks)
+        raise_error(ctrl, FLRL_E_ARG);
 }
 
 // Decode: persistent 512-thread workgroups (kDecPerCU per CU) take 64 KiB
@@ -651,152 +519,139 @@ __device__ __forceinline__ uint64_t dec_load_widths(const uint8_t *bits, uint64_
 template <int ITEMS>
 __global__ __launch_bounds__(kDecThreads, kDecPerCU) void fl_decode_kernel(
     const uint8_t *__restrict__ bits, uint64_t nframes, const uint8_t *__restrict__ values,
-    uint64_t vsize, uint8_t *__restrict__ out, uint64_t n, uint64_t *tile_base, uint32_t ntiles,
-    uint32_t TB, uint32_t nblocks, uint64_t *status, uint64_t help_ticks, Ctrl *ctrl)
+    uint64_t vsize, uint8_t *__restrict__ out, uint64_t n, const uint64_t *__restrict__ tile_base,
+    uint32_t ntiles, Ctrl *ctrl, uint32_t ticket0)
 {
     static_assert(ITEMS == 8, "a lane group's widths are one u64");
     constexpr int T = kDecThreads;
-    constexpr int TB_BYTES = T * 16 * ITEMS;
-    constexpr int TF = TB_BYTES / kFrame;
-    __shared__ u32x4 s_in[TB_BYTES / 16 + 2];  // +2: a lane may read up to 18 bytes past its frame
+    constexpr int TB = T * 16 * ITEMS;
+    constexpr int TF = TB / kFrame;
+    __shared__ u32x4 s_in[TB / 16 + 2];  // +2: a lane may read up to 18 bytes past its frame
     __shared__ uint32_t s_wave[T / kWave];
-    __shared__ uint32_t s_wave2[2 * (T / kWave)];
-    __shared__ uint64_t s_red[T / kWave];
     __shared__ uint32_t s_next[2];  // alternating: a slot is rewritten two barriers after its read
     const int tid = threadIdx.x;
     const int lane = tid & (kWave - 1);
     const int wave = tid / kWave;
-
-    // ---- phase 1: the offsets of this workgroup's blocks (one per workgroup
-    // up to 1 GiB; more in workgroup-index order past that)
-    for (uint32_t blk = blockIdx.x; blk < nblocks; blk += gridDim.x)
-        fl_decode_offsets<T>(bits, nframes, vsize, n, tile_base, ntiles, blk, TB, status, help_ticks, ctrl,
-                             s_wave2, s_red);
-    const DecOffsets P{bits, nframes, vsize, n, tile_base, status, ntiles, TB, help_ticks, s_wave2, s_red};
-    if (blockIdx.x < ntiles)
-        dec_wait_blocks(P, nblocks, ctrl, &s_next[0]);
-
-    // ---- phase 2: decode. The first two tiles are grid-stride (no atomic
-    // round trip at the launch, when every workgroup would queue on the counter
-    // at once: -3.4 us, and -1 % more for the second); later tiles by ticket,
-    // numbered past them: workgroups progress through the output in order
-    const uint32_t ticket0 = 2u * gridDim.x;
-    bool first_round = true;
+    // the first two tiles are grid-stride (no atomic round trip at the launch,
+    // when every workgroup would queue on the counter at once: -3.4 us, and
+    // -1 % more for the second); later tiles by ticket, numbered past them
+    // (ticket0: tickets the pre-pass took from the same counter, now none):
+    // workgroups progress through the output in order
+    ticket0 -= 2u * gridDim.x;
+    bool first_round = true;  // the second tile is grid-stride too (-1 %: no burst of tickets at the start)
     uint32_t tile = blockIdx.x;
     uint32_t slot = 1;
-    uint64_t base = 0;
-    uint32_t agg = 0;
-    if (tile < ntiles && tile_span(P, tile, base, agg, ctrl)) {
-        u32x4 a[ITEMS];
-        dec_load_values<ITEMS>(a, values, base, agg, vsize);
-        uint64_t wv = dec_load_widths(bits, (uint64_t)tile * TF + (tid >> 3) * ITEMS, nframes);
-        for (;;) {
-            if (tid == 0)  // read after the scan barrier below
-                s_next[slot] = first_round ? tile + gridDim.x : atomicAdd(&ctrl->ticket, 1u) + ticket0;
-            first_round = false;
+    if (tile >= ntiles)
+        return;
+    // a pre-pass that raised (a stale ticket leaves tile_base unwritten) ends
+    // the decode before any offset is used; loaded beside the first offsets
+    const uint32_t err = __hip_atomic_load(&ctrl->error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint64_t base = tile_base[tile];
+    uint32_t agg = (uint32_t)(tile_base[tile + 1] - base);
+    if (err != 0)
+        return;
+    u32x4 a[ITEMS];
+    dec_load_values<ITEMS>(a, values, base, agg, vsize);
+    uint64_t wv = dec_load_widths(bits, (uint64_t)tile * TF + (tid >> 3) * ITEMS, nframes);
+    for (;;) {
+        if (tid == 0)  // read after the scan barrier below
+            s_next[slot] = first_round ? tile + gridDim.x : atomicAdd(&ctrl->ticket, 1u) - ticket0;
+        first_round = false;
 #pragma unroll
-            for (int k = 0; k < ITEMS; ++k)
-                if ((uint32_t)(k * T + tid) < agg)
-                    s_in[k * T + tid] = a[k];
-            if (tid < 2)
-                s_in[agg + tid] = u32x4{0u, 0u, 0u, 0u};
-            // widths (clamped as phase 1 clamps them; 0 past the last frame)
-            uint32_t bw[ITEMS];
-            uint32_t gtot = 0;
+        for (int k = 0; k < ITEMS; ++k)
+            if ((uint32_t)(k * T + tid) < agg)
+                s_in[k * T + tid] = a[k];
+        if (tid < 2)
+            s_in[agg + tid] = u32x4{0u, 0u, 0u, 0u};
+        // widths (clamped as fl_offsets_kernel clamps them; 0 past the last frame)
+        uint32_t bw[ITEMS];
+        uint32_t gtot = 0;
 #pragma unroll
-            for (int k = 0; k < ITEMS; ++k) {
-                const uint64_t f = (uint64_t)tile * TF + (tid >> 3) * ITEMS + k;
-                const uint32_t b = f < nframes ? clamp_width((uint32_t)(wv >> (8 * k)) & 0xFFu) : 0u;
-                bw[k] = b;
-                gtot += b;
-            }
-            const uint32_t gincl = wave_incl_scan_u32((lane & 7) == 0 ? gtot : 0u);
-            if (lane == kWave - 1)
-                s_wave[wave] = gincl;
-            __syncthreads();
-            uint32_t wbase = 0;
-#pragma unroll
-            for (int v = 0; v < T / kWave; ++v)
-                wbase += v < wave ? s_wave[v] : 0u;
-
-            // ---- next tile's loads, in flight while this tile is unpacked
-            const uint32_t nxt = s_next[slot];
-            slot ^= 1u;
-            bool more = nxt < ntiles;
-            const uint64_t tile_off = (uint64_t)tile * TB_BYTES;
-            if (more) {
-                more = tile_span(P, nxt, base, agg, ctrl);
-                if (more) {
-                    dec_load_values<ITEMS>(a, values, base, agg, vsize);
-                    wv = dec_load_widths(bits, (uint64_t)nxt * TF + (tid >> 3) * ITEMS, nframes);
-                }
-            }
-
-            // ---- unpack 2b bytes -> 16 values per lane and item, store
-            const uint32_t *s32 = reinterpret_cast<const uint32_t *>(s_in);
-            const bool full = tile_off + TB_BYTES <= n;
-            uint32_t run = wbase + gincl - gtot;  // widths before this group's first frame
-            uint8_t *dst = out + tile_off + (uint32_t)(tid >> 3) * ITEMS * kFrame + (tid & 7) * 16;
-#pragma unroll
-            for (int k = 0; k < ITEMS; ++k) {
-                const uint32_t b = bw[k];
-                const uint32_t off = 16u * run + 2u * b * (uint32_t)(tid & 7);
-                run += b;
-                if (b == 0)
-                    continue;
-                const uint32_t ad = off >> 2;
-                const uint64_t w01 = ((uint64_t)s32[ad + 1] << 32) | s32[ad];
-                const uint64_t w23 = ((uint64_t)s32[ad + 3] << 32) | s32[ad + 2];
-                uint64_t lo = w01, hi = w23;
-                if (off & 2) {  // 2-byte aligned start: funnel by 16 bits
-                    const uint64_t w4 = s32[ad + 4];
-                    lo = (w01 >> 16) | (w23 << 48);
-                    hi = (w23 >> 16) | (w4 << 48);
-                }
-                const uint64_t p1 = b == 8 ? hi : ((lo >> (8 * b)) | (hi << (64 - 8 * b)));
-                const uint64_t x0 = unpack8(lo, b);
-                const uint64_t x1 = unpack8(p1, b);
-                const u32x4 r = u32x4{(uint32_t)x0, (uint32_t)(x0 >> 32), (uint32_t)x1,
-                                      (uint32_t)(x1 >> 32)};
-                if (full)
-                    __builtin_nontemporal_store(r, reinterpret_cast<u32x4 *>(dst + k * kFrame));
-                else
-                    store16_tail(out, (uint64_t)(dst - out) + k * kFrame, n, r);
-            }
-            if (!more)
-                break;
-            tile = nxt;
-            __syncthreads();  // every wave is done reading s_in / s_wave / s_next
+        for (int k = 0; k < ITEMS; ++k) {
+            const uint64_t f = (uint64_t)tile * TF + (tid >> 3) * ITEMS + k;
+            const uint32_t b = f < nframes ? clamp_width((uint32_t)(wv >> (8 * k)) & 0xFFu) : 0u;
+            bw[k] = b;
+            gtot += b;
         }
+        const uint32_t gincl = wave_incl_scan_u32((lane & 7) == 0 ? gtot : 0u);
+        if (lane == kWave - 1)
+            s_wave[wave] = gincl;
+        __syncthreads();
+        uint32_t wbase = 0;
+#pragma unroll
+        for (int v = 0; v < T / kWave; ++v)
+            wbase += v < wave ? s_wave[v] : 0u;
+
+        // ---- next tile's loads, in flight while this tile is unpacked
+        const uint32_t nxt = s_next[slot];
+        slot ^= 1u;
+        const bool more = nxt < ntiles;
+        const uint64_t tile_off = (uint64_t)tile * TB;
+        if (more) {
+            base = tile_base[nxt];
+            agg = (uint32_t)(tile_base[nxt + 1] - base);
+            dec_load_values<ITEMS>(a, values, base, agg, vsize);
+            wv = dec_load_widths(bits, (uint64_t)nxt * TF + (tid >> 3) * ITEMS, nframes);
+        }
+
+        // ---- unpack 2b bytes -> 16 values per lane and item, store
+        const uint32_t *s32 = reinterpret_cast<const uint32_t *>(s_in);
+        const bool full = tile_off + TB <= n;
+        uint32_t run = wbase + gincl - gtot;  // widths before this group's first frame
+        uint8_t *dst = out + tile_off + (uint32_t)(tid >> 3) * ITEMS * kFrame + (tid & 7) * 16;
+#pragma unroll
+        for (int k = 0; k < ITEMS; ++k) {
+            const uint32_t b = bw[k];
+            const uint32_t off = 16u * run + 2u * b * (uint32_t)(tid & 7);
+            run += b;
+            if (b == 0)
+                continue;
+            const uint32_t ad = off >> 2;
+            const uint64_t w01 = ((uint64_t)s32[ad + 1] << 32) | s32[ad];
+            const uint64_t w23 = ((uint64_t)s32[ad + 3] << 32) | s32[ad + 2];
+            uint64_t lo = w01, hi = w23;
+            if (off & 2) {  // 2-byte aligned start: funnel by 16 bits
+                const uint64_t w4 = s32[ad + 4];
+                lo = (w01 >> 16) | (w23 << 48);
+                hi = (w23 >> 16) | (w4 << 48);
+            }
+            const uint64_t p1 = b == 8 ? hi : ((lo >> (8 * b)) | (hi << (64 - 8 * b)));
+            const uint64_t x0 = unpack8(lo, b);
+            const uint64_t x1 = unpack8(p1, b);
+            const u32x4 r = u32x4{(uint32_t)x0, (uint32_t)(x0 >> 32), (uint32_t)x1,
+                                  (uint32_t)(x1 >> 32)};
+            if (full)
+                __builtin_nontemporal_store(r, reinterpret_cast<u32x4 *>(dst + k * kFrame));
+            else
+                store16_tail(out, (uint64_t)(dst - out) + k * kFrame, n, r);
+        }
+        if (!more)
+            break;
+        tile = nxt;
+        __syncthreads();  // every wave is done reading s_in / s_wave / s_next
     }
-    // a launch counts exactly gridDim.x arrivals on the reset counter: more
-    // means the scratch was not reset for it (its tickets, status words and
-    // tagged offsets were stale too, so the output is not trusted)
-    if (tid == 0 && atomicAdd(reinterpret_cast<uint32_t *>(&ctrl->aux), 1u) >= gridDim.x)
-        raise_error(ctrl, FLRL_E_ARG);
 }
 
 // ---- scratch layout ---------------------------------------------------------
-// [Ctrl 16 B][encode: status lines[enc_tiles]]   or
-// [Ctrl 16 B][decode: status lines[dec_blocks]][tile_base[dec_tiles + 1]]
-// all zeroed per call (the decode's tile_base holds tagged granules). Offsets
-// blocks of dec_tb tiles: one per decode workgroup (2 per CU x 256 CUs) up to
-// 2 GiB, 64 tiles (4 MiB of output) each past that.
-constexpr size_t kDecBlocksTarget = 512;
+// [Ctrl 16 B][encode: status[enc_tiles]]   or
+// [Ctrl 16 B][decode: status lines[off_blocks]][tile_base[dec_tiles + 1]]
+// Only Ctrl + status are zeroed per call.
 struct FlLayout {
-    size_t enc_tiles, dec_tiles, dec_tb, dec_blocks;
+    size_t enc_tiles, dec_tiles, off_blocks, off_iters;
     size_t enc_zero, dec_zero, bytes;
     explicit FlLayout(size_t n)
     {
+        const size_t frames = div_up(n, kFrame);
         enc_tiles = div_up(n, (size_t)kEncTileBytes);
         dec_tiles = div_up(n, (size_t)kDecTileBytes);
-        dec_tb = div_up(dec_tiles, kDecBlocksTarget);
-        dec_tb = dec_tb < 1 ? 1 : (dec_tb > (size_t)kDecTilesPerRound * kDecBlockRounds
-                                       ? (size_t)kDecTilesPerRound * kDecBlockRounds : dec_tb);
-        dec_blocks = div_up(dec_tiles, dec_tb);
+        // offsets rounds per workgroup: the grid stays within kMaxPrefixBlocks
+        off_iters = div_up(div_up(frames, (size_t)kOffFrames), (size_t)kMaxPrefixBlocks);
+        off_iters = off_iters ? off_iters : 1;
+        off_blocks = div_up(frames, (size_t)kOffFrames * off_iters);
         enc_zero = FLRL_FL_STATUS_OFF + round_up(enc_tiles * 8 * FLRL_FL_STATUS_STRIDE, 16);
-        dec_zero = sizeof(Ctrl) + dec_blocks * 8 * kDecStatusStride + round_up((dec_tiles + 1) * 8, 16);
-        bytes = enc_zero > dec_zero ? enc_zero : dec_zero;
+        dec_zero = sizeof(Ctrl) + off_blocks * 8 * kOffStatusStride;
+        const size_t dec_bytes = dec_zero + round_up((dec_tiles + 1) * 8, 16);
+        bytes = enc_zero > dec_bytes ? enc_zero : dec_bytes;
     }
 };
 
@@ -875,15 +730,19 @@ extern "C" int flrl_fl_decode_device(const uint8_t *d_bits, size_t bits_size,
     FLRL_HIP(scratch_reset(d_scratch, L.dec_zero, s));
     Ctrl *ctrl = static_cast<Ctrl *>(d_scratch);
     uint64_t *status = reinterpret_cast<uint64_t *>(ctrl + 1);
-    uint64_t *tile_base = reinterpret_cast<uint64_t *>(static_cast<uint8_t *>(d_scratch) + sizeof(Ctrl) +
-                                                       L.dec_blocks * 8 * kDecStatusStride);
+    uint64_t *tile_base =
+        reinterpret_cast<uint64_t *>(static_cast<uint8_t *>(d_scratch) + L.dec_zero);
+    hipLaunchKernelGGL(fl_offsets_kernel, dim3((uint32_t)L.off_blocks), dim3(kThreads), 0, s,
+                       d_bits, (uint64_t)bits_size, (uint64_t)values_size, (uint64_t)n, tile_base,
+                       (uint32_t)L.dec_tiles, (uint32_t)L.off_blocks, (uint32_t)L.off_iters, ctrl, status,
+                       lookback_help_ticks(kFlHelpTicks));
+    FLRL_HIP(hipGetLastError());
     const size_t dgrid = (size_t)kDecPerCU * (size_t)cu_count();
     kernel_timing_begin(s);
     hipLaunchKernelGGL(fl_decode_kernel<kDecItems>,
                        dim3((uint32_t)(L.dec_tiles < dgrid ? L.dec_tiles : dgrid)), dim3(kDecThreads), 0,
                        s, d_bits, (uint64_t)bits_size, d_values, (uint64_t)values_size, d_out,
-                       (uint64_t)n, tile_base, (uint32_t)L.dec_tiles, (uint32_t)L.dec_tb,
-                       (uint32_t)L.dec_blocks, status, lookback_help_ticks(kFlHelpTicks), ctrl);
+                       (uint64_t)n, tile_base, (uint32_t)L.dec_tiles, ctrl, 0u);
     kernel_timing_end(s);
     FLRL_HIP(hipGetLastError());
     return FLRL_OK;

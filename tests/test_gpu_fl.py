@@ -490,11 +490,11 @@ def test_concurrent_streams():
 @pytest.mark.gpu
 @pytest.mark.parametrize("n", [(48 << 20) + 5, 1 << 30, 100_003])
 def test_decode_offsets_fallback_bit_exact(n):
-    """The FL decode computes its tile offsets in-kernel (phase 1, one block of
-    tiles per workgroup); a block whose owner has not started is computed by
-    a waiting workgroup after a timeout (the decoupled fallback: other kernels
-    can hold the CUs). flrl_debug_lookback_help_us(0) takes the fallback at
-    every wait: the decode must stay bit-exact and error-free."""
+    """The FL decode pre-pass numbers its blocks by workgroup index and waits
+    for every predecessor block's aggregate; one whose workgroup has not
+    started (other kernels holding the CUs) is computed from its widths after
+    a timeout (the decoupled fallback). flrl_debug_lookback_help_us(0) takes
+    the fallback at every wait: the decode must stay bit-exact and error-free."""
     import flrl
     from flrl.device import FLDevice, gen
     x = gen("lo4", n, 5)
