@@ -313,65 +313,6 @@ __device__ __forceinline__ uint64_t block_prefix_all(uint64_t *status, uint32_t 
     return excl;
 }
 
-// block_prefix_all for workgroups numbered by INDEX instead of a ticket (the
-// pre-passes' tickets queued every workgroup of the launch on one counter):
-// the dispatcher starts a launch's workgroups in index order on each XCD, so an
-// unpublished predecessor is running or about to start -- unless other kernels
-// hold the CUs while waiting on their own unstarted workgroups; a word still
-// unpublished after help_ticks (s_memrealtime) is computed by the waiting
-// thread, help(j), from the predecessor's input (per thread, no barrier inside).
-// Status words one per 128-byte line (stride S granules): every workgroup
-// reads every predecessor's word.
-template <int T, int S, class Help>
-__device__ __forceinline__ uint64_t block_prefix_all_help(uint64_t *status, uint32_t blk, uint64_t agg,
-                                                          Ctrl *ctrl, uint64_t *s_red, uint64_t help_ticks,
-                                                          Help &&help)
-{
-    const int tid = threadIdx.x;
-    if (tid == 0)
-        granule_store(&status[(size_t)blk * S], kFlagA | agg);
-    uint64_t sum = 0;
-    for (uint32_t j0 = 0; j0 < blk; j0 += 4 * T) {
-        uint64_t g[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const uint32_t j = j0 + (uint32_t)tid + (uint32_t)k * T;
-            g[k] = j < blk ? granule_load(&status[(size_t)j * S]) : kFlagA;
-        }
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const uint32_t j = j0 + (uint32_t)tid + (uint32_t)k * T;
-            uint64_t t0 = 0;
-            uint32_t spins = 0;
-            while ((g[k] >> 62) == 0) {
-                const uint64_t now = __builtin_amdgcn_s_memrealtime();
-                if (t0 == 0)
-                    t0 = now;
-                if (now - t0 >= help_ticks) {
-                    g[k] = kFlagA | help(j);
-                    break;
-                }
-                if (++spins > kSpinLimit) {
-                    raise_error(ctrl, FLRL_E_TIMEOUT);
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(1);
-                g[k] = granule_load(&status[(size_t)j * S]);
-            }
-            sum += g[k] & kPayload;
-        }
-    }
-    sum = wave_sum_u64(sum);
-    if ((tid & (kWave - 1)) == 0)
-        s_red[tid / kWave] = sum;
-    __syncthreads();
-    uint64_t excl = 0;
-#pragma unroll
-    for (int v = 0; v < T / kWave; ++v)
-        excl += s_red[v];
-    return excl;
-}
-
 // 16-byte load of bytes [o, o+16) of p (o and p 16-byte aligned), zero-filling
 // past n. A straddling chunk is read whole: a 16-byte-aligned block never
 // crosses a page, so this cannot fault; the bytes at or past n are masked off.

@@ -57,8 +57,6 @@ constexpr int kDecItems = 8;      // decode tile = 512 lanes x 8 x 16 B = 64 KiB
 constexpr int kDecPerCU = 2;      // persistent decode workgroups per CU (LDS 64 KiB each)
 constexpr int kDecTileBytes = kDecThreads * 16 * kDecItems;
 constexpr int kDecTileFrames = kDecTileBytes / kFrame;
-constexpr int kOffStatusStride = FLRL_FL_OFF_STATUS_STRIDE;  // pre-pass status granules per block (one line)
-constexpr uint64_t kFlHelpTicks = 20000;  // pre-pass: a predecessor unpublished for 200 us is computed
 constexpr int kOffFramesPerThread = 128;  // (64: 1 GiB decode call +1 %, more workgroups to scan; 256: equal)
 constexpr int kOffFrames = kThreads * kOffFramesPerThread;  // frames per offsets workgroup
 constexpr int kOffLanesPerTile = kDecTileFrames / kOffFramesPerThread;  // offsets lanes per decode tile
@@ -334,43 +332,32 @@ __global__ __launch_bounds__(T + kWave, 1) void fl_encode_kernel(
     }
 }
 
-// Clamped widths of the 16 frames at f (f % 16 == 0; frames at or past nframes
-// count 0): the decoupled fallback's sum of a predecessor block.
-__device__ __forceinline__ uint64_t sum_widths(const uint8_t *bits, uint64_t fa, uint64_t fb)
-{
-    uint64_t h = 0;
-    for (uint64_t f = fa; f < fb; f += 16) {
-        const u32x4 q = load16_tail(bits, f, fb);
-        for (int i = 0; i < 16 && f + i < fb; ++i)
-            h += clamp_width((q[i >> 2] >> (8 * (i & 3))) & 0xFFu);
-    }
-    return h;
-}
-
 // Decode pre-pass: one workgroup scans `iters` x kOffFrames frame widths (64
 // per lane per round), validates them (a width outside [1,8] raises
 // FLRL_E_FORMAT and is clamped, as fl_decode_kernel clamps it, so offsets stay
 // consistent and in bounds), and writes the output offset (16-byte units) of
 // each 256-frame decode tile: tile_base[t] for t < ntiles and tile_base[ntiles]
 // = total. Offsets are first written workgroup-relative; once the workgroup's
-// base is known (block_prefix_all_help: iters keeps the grid within
+// base is known (block_prefix_all: iters keeps the grid within
 // kMaxPrefixBlocks) each lane adds it to the entries it wrote. The workgroup
-// holding the last frame checks valuesSize against the widths. Blocks are
-// numbered by workgroup index (a ticket per workgroup queued the whole launch
-// on one counter at its start), with the decoupled fallback of
-// block_prefix_all_help; a launch counts exactly nblocks arrivals on the reset
-// counter (Ctrl::aux), more means its scratch was not reset.
+// holding the last frame checks valuesSize against the widths.
 __global__ __launch_bounds__(kThreads) void fl_offsets_kernel(
     const uint8_t *__restrict__ bits, uint64_t nframes, uint64_t vsize, uint64_t n,
     uint64_t *__restrict__ tile_base, uint32_t ntiles, uint32_t nblocks, uint32_t iters, Ctrl *ctrl,
-    uint64_t *status, uint64_t help_ticks)
+    uint64_t *status)
 {
     __shared__ uint32_t s_wave[kWaves];
+    __shared__ uint32_t s_ticket;
     __shared__ uint64_t s_red[kWaves];
     const int tid = threadIdx.x;
     const int lane = tid & (kWave - 1);
     const int wave = tid / kWave;
-    const uint32_t blk = blockIdx.x;
+    const uint32_t blk = take_ticket(ctrl, &s_ticket);
+    if (blk >= nblocks) {  // the scratch's ticket was not reset for this launch
+        if (threadIdx.x == 0)
+            raise_error(ctrl, FLRL_E_ARG);
+        return;
+    }
     uint64_t local = 0;          // frames' 16-byte units before this round, workgroup-relative
     bool has_last = false;       // this lane holds the last frame
     uint64_t last_local = 0;     // its units before the last frame, workgroup-relative
@@ -447,13 +434,7 @@ __global__ __launch_bounds__(kThreads) void fl_offsets_kernel(
     }
     if (bad)
         raise_error(ctrl, FLRL_E_FORMAT);
-    const uint64_t block_frames = (uint64_t)iters * kOffFrames;
-    auto help = [&](uint32_t j) -> uint64_t {  // block j's aggregate from its widths
-        const uint64_t fa = (uint64_t)j * block_frames;
-        return sum_widths(bits, fa, fa + block_frames < nframes ? fa + block_frames : nframes);
-    };
-    const uint64_t base =
-        block_prefix_all_help<kThreads, kOffStatusStride>(status, blk, local, ctrl, s_red, help_ticks, help);
+    const uint64_t base = block_prefix_all<kThreads>(status, blk, local, ctrl, s_red);
     for (uint32_t it = 0; it < iters; ++it) {
         const uint64_t f0 = ((uint64_t)blk * iters + it) * kOffFrames + (uint64_t)tid * kOffFramesPerThread;
         const uint64_t tile = f0 / kDecTileFrames;
@@ -469,8 +450,6 @@ __global__ __launch_bounds__(kThreads) void fl_offsets_kernel(
         if (expect != vsize)
             raise_error(ctrl, FLRL_E_FORMAT);
     }
-    if (tid == 0 && atomicAdd(reinterpret_cast<uint32_t *>(&ctrl->aux), 1u) >= nblocks)
-        raise_error(ctrl, FLRL_E_ARG);
 }
 
 // Decode: persistent 512-thread workgroups (kDecPerCU per CU) take 64 KiB
@@ -535,8 +514,8 @@ __global__ __launch_bounds__(kDecThreads, kDecPerCU) void fl_decode_kernel(
     // the first two tiles are grid-stride (no atomic round trip at the launch,
     // when every workgroup would queue on the counter at once: -3.4 us, and
     // -1 % more for the second); later tiles by ticket, numbered past them
-    // (ticket0: tickets the pre-pass took from the same counter, now none):
-    // workgroups progress through the output in order
+    // (fl_offsets_kernel's workgroups took tickets 0..ticket0-1 of the same
+    // counter): workgroups progress through the output in order
     ticket0 -= 2u * gridDim.x;
     bool first_round = true;  // the second tile is grid-stride too (-1 %: no burst of tickets at the start)
     uint32_t tile = blockIdx.x;
@@ -634,7 +613,7 @@ __global__ __launch_bounds__(kDecThreads, kDecPerCU) void fl_decode_kernel(
 
 // ---- scratch layout ---------------------------------------------------------
 // [Ctrl 16 B][encode: status[enc_tiles]]   or
-// [Ctrl 16 B][decode: status lines[off_blocks]][tile_base[dec_tiles + 1]]
+// [Ctrl 16 B][decode: status[off_blocks] (16-B padded)][tile_base[dec_tiles + 1]]
 // Only Ctrl + status are zeroed per call.
 struct FlLayout {
     size_t enc_tiles, dec_tiles, off_blocks, off_iters;
@@ -649,7 +628,7 @@ struct FlLayout {
         off_iters = off_iters ? off_iters : 1;
         off_blocks = div_up(frames, (size_t)kOffFrames * off_iters);
         enc_zero = FLRL_FL_STATUS_OFF + round_up(enc_tiles * 8 * FLRL_FL_STATUS_STRIDE, 16);
-        dec_zero = sizeof(Ctrl) + off_blocks * 8 * kOffStatusStride;
+        dec_zero = sizeof(Ctrl) + round_up(off_blocks * 8, 16);
         const size_t dec_bytes = dec_zero + round_up((dec_tiles + 1) * 8, 16);
         bytes = enc_zero > dec_bytes ? enc_zero : dec_bytes;
     }
@@ -734,15 +713,14 @@ extern "C" int flrl_fl_decode_device(const uint8_t *d_bits, size_t bits_size,
         reinterpret_cast<uint64_t *>(static_cast<uint8_t *>(d_scratch) + L.dec_zero);
     hipLaunchKernelGGL(fl_offsets_kernel, dim3((uint32_t)L.off_blocks), dim3(kThreads), 0, s,
                        d_bits, (uint64_t)bits_size, (uint64_t)values_size, (uint64_t)n, tile_base,
-                       (uint32_t)L.dec_tiles, (uint32_t)L.off_blocks, (uint32_t)L.off_iters, ctrl, status,
-                       lookback_help_ticks(kFlHelpTicks));
+                       (uint32_t)L.dec_tiles, (uint32_t)L.off_blocks, (uint32_t)L.off_iters, ctrl, status);
     FLRL_HIP(hipGetLastError());
     const size_t dgrid = (size_t)kDecPerCU * (size_t)cu_count();
     kernel_timing_begin(s);
     hipLaunchKernelGGL(fl_decode_kernel<kDecItems>,
                        dim3((uint32_t)(L.dec_tiles < dgrid ? L.dec_tiles : dgrid)), dim3(kDecThreads), 0,
                        s, d_bits, (uint64_t)bits_size, d_values, (uint64_t)values_size, d_out,
-                       (uint64_t)n, tile_base, (uint32_t)L.dec_tiles, ctrl, 0u);
+                       (uint64_t)n, tile_base, (uint32_t)L.dec_tiles, ctrl, (uint32_t)L.off_blocks);
     kernel_timing_end(s);
     FLRL_HIP(hipGetLastError());
     return FLRL_OK;

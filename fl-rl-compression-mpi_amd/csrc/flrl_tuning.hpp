@@ -12,7 +12,7 @@
 #if !defined(FLRL_TUNING_BUILD) &&                                                                  \
     (defined(FLRL_RL_TRACE) || defined(FLRL_RL_LB_STAT) || defined(FLRL_FL_TRACE) ||                \
      defined(FLRL_RL_THREADS) || defined(FLRL_RD_TICKET_MIN) || defined(FLRL_FL_LOOKG) || defined(FLRL_FL_LOOKL) ||\
-     defined(FLRL_FL_STATUS_STRIDE) || defined(FLRL_FL_OFF_STATUS_STRIDE) || defined(FLRL_FL_STATUS_OFF) || defined(FLRL_RL_LOOKL) || defined(FLRL_RL_LOOKG) || defined(FLRL_RL_PF) ||\
+     defined(FLRL_FL_STATUS_STRIDE) || defined(FLRL_FL_STATUS_OFF) || defined(FLRL_RL_LOOKL) || defined(FLRL_RL_LOOKG) || defined(FLRL_RL_PF) ||\
      defined(FLRL_RL_STATUS_STRIDE) || defined(FLRL_RL_STATUS_OFF) ||\
      defined(FLRL_RL_STAGE) || defined(FLRL_RL_WPS) || defined(FLRL_RD_NARROW_MEAN) || defined(FLRL_RL_RO_MAXB) ||          \
      defined(FLRL_RD_UNROLL) || defined(FLRL_HOST_WORKERS) || defined(FLRL_HOST_CHUNK) ||                \
@@ -53,9 +53,6 @@
 #ifndef FLRL_FL_STATUS_OFF
 #define FLRL_FL_STATUS_OFF 256  // FL encode status array offset (Ctrl with the ticket on its own lines)
 #endif
-#ifndef FLRL_FL_OFF_STATUS_STRIDE
-#define FLRL_FL_OFF_STATUS_STRIDE 16  // FL decode pre-pass blocks: one 128-B status line each
-#endif
 #ifndef FLRL_RD_TICKET_MIN
 #define FLRL_RD_TICKET_MIN 3  // RL block decode: tiles by ticket from this many tiles per workgroup on (2: 256 MiB +3 %)
 #endif
@@ -77,7 +74,7 @@
 
 // RL encode: sub-chunks in flight per wave during the scan (register sets)
 #ifndef FLRL_RL_PF
-#define FLRL_RL_PF 1
+#define FLRL_RL_PF 2  // (1 GiB, ab_libs: runs32 -1.2 %, long runs -2.4 %, all-zero -3 %; random bytes +2 %, runs of 1..12 +2 %)
 #endif
 
 // RL encode: minimum waves per SIMD the kernels are compiled for (5: five

@@ -486,28 +486,3 @@ def test_concurrent_streams():
             assert torch.equal(rl[i].counts[:R], c0) and torch.equal(rl[i].values[:R], rv0), (rep, i)
             assert torch.equal(rl[i].out[: sizes[2 + i]], xs[2 + i][: sizes[2 + i]]), (rep, i)
 
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("n", [(48 << 20) + 5, 1 << 30, 100_003])
-def test_decode_offsets_fallback_bit_exact(n):
-    """The FL decode pre-pass numbers its blocks by workgroup index and waits
-    for every predecessor block's aggregate; one whose workgroup has not
-    started (other kernels holding the CUs) is computed from its widths after
-    a timeout (the decoupled fallback). flrl_debug_lookback_help_us(0) takes
-    the fallback at every wait: the decode must stay bit-exact and error-free."""
-    import flrl
-    from flrl.device import FLDevice, gen
-    x = gen("lo4", n, 5)
-    x[n // 3] = 0xFF
-    d = FLDevice(n)
-    d.encode(x)
-    v = d.values_size()
-    flrl.debug_lookback_help_us(0)
-    try:
-        for _ in range(3):
-            out = d.decode(v)
-            torch.cuda.synchronize()
-            assert d.error() == 0
-            assert torch.equal(out, x[:n])
-    finally:
-        flrl.debug_lookback_help_us(-1)
