@@ -19,7 +19,7 @@
 // then the packed tile streams out in coalesced 16-byte stores (offsets are
 // multiples of 16). HBM loads of tile t+1 are in flight across tile t's
 // look-back and stores. Tile size, workgroup shape and the look-back ordering
-// were chosen by measurement (scripts/ubench_encode.hip, scripts/ab_encode.py,
+// were chosen by measurement (round-1/2 harness ubench_encode.hip, scripts/ab_encode.py,
 // DESIGN.md §Encode).
 //
 // Decode is two launches: fl_offsets_kernel scans the frame widths (F bytes,
@@ -458,7 +458,7 @@ __global__ __launch_bounds__(kThreads) void fl_offsets_kernel(
 // scan, while the current tile is unpacked from LDS. Lane group g = tid/8 owns
 // frames g*ITEMS .. +ITEMS-1 of the tile (its prefix is a register running sum
 // after one wave scan); lane tid%8 unpacks 16-byte chunk tid%8 of each.
-// Measured against one 32 KiB tile per workgroup (scripts/ubench_decode.hip):
+// Measured against one 32 KiB tile per workgroup (round-1/2 harness ubench_decode.hip):
 // -6 % at 1 GiB u8, -5 % lo4, -13 % at 16 GiB. Grid-stride tiles instead of
 // tickets were as good at 1 GiB but 10 % slower at 16 GiB (workgroups drift
 // apart in the address space); 32 KiB tiles by ticket saturate the ticket

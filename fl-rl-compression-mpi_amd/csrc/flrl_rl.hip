@@ -1213,6 +1213,15 @@ __global__ __launch_bounds__(kRoThreads, 4) void rl_offsets_kernel(  // 4 workgr
 // in bytes 1..i), gathered with byte permutes. (Gathering from the 16 values
 // from run r on took three permutes per dword; two 8-value windows take one:
 // VALU instructions -25 %, 1 GiB runs32 kernel -2..6 %.)
+// Slot of byte-prefix table entry x. A ds_read_b64 serves 32 lanes per LDS
+// cycle, entry slot s on banks 2s, 2s+1 (mod 64): plain slots put entries 0,
+// 32, 64 and 128 on one bank pair, and with sparse start masks (runs32: a start
+// every other chunk) those are most of the lookups -- ~5.5 LDS cycles per
+// lookup instead of 2 in a model of runs32 masks; three padding slots per 32
+// entries spread the single-bit entries over distinct banks (~2.2).
+constexpr int kPfxSlots = 256 + 3 * 7 + 1;
+__device__ __forceinline__ uint32_t pfx_slot(uint32_t x) { return x + 3u * (x >> 5); }
+
 __device__ __forceinline__ u32x4 rd_chunk(const uint32_t *bm, const uint32_t *pre, const uint32_t *v32,
                                           const uint64_t *pfx, uint32_t q, uint32_t before)
 {
@@ -1236,7 +1245,7 @@ __device__ __forceinline__ u32x4 rd_chunk(const uint32_t *bm, const uint32_t *pr
     const uint32_t r8 = (uint32_t)r + (uint32_t)__popc(m1 & 0x1FFu);
     const uint32_t a8 = r8 >> 2, sh8 = r8 & 3u;
     const uint32_t e0 = v32[a8], e1 = v32[a8 + 1], e2 = v32[a8 + 2];
-    const uint64_t klo = pfx[m1 & 0xFFu], khi = pfx[(m1 >> 8) & 0xFEu];
+    const uint64_t klo = pfx[pfx_slot(m1 & 0xFFu)], khi = pfx[pfx_slot((m1 >> 8) & 0xFEu)];
     const uint32_t w0 = __builtin_amdgcn_alignbyte(d1, d0, sh);
     const uint32_t w1 = __builtin_amdgcn_alignbyte(d2, d1, sh);
     const uint32_t u0 = __builtin_amdgcn_alignbyte(e1, e0, sh8);
@@ -1294,7 +1303,7 @@ __global__ __launch_bounds__(T, 4) void rl_decode_kernel(  // 2nd: waves per SIM
     __shared__ u32x4 s_big4[(2 * kRkWords + kRdRuns + 1 + 3) / 4];
     __shared__ u32x4 s_val4[kRdRuns / 16 + 1];  // +16 B: the permute window reads up to 19 bytes past a run
     __shared__ uint32_t s_wave[T / kWave];
-    __shared__ uint64_t s_pfx[256];  // byte i of s_pfx[x] = popcount(x & ((2 << i) - 1))
+    __shared__ uint64_t s_pfx[kPfxSlots];  // byte i of s_pfx[pfx_slot(x)] = popcount(x & ((2 << i) - 1))
     static_assert(sizeof(s_big4) >= kRkDense, "dense window fits the aliased LDS");
     u32x4 *const s_bm4 = s_big4;
     uint32_t *const s_bm = reinterpret_cast<uint32_t *>(s_big4);
@@ -1324,7 +1333,7 @@ __global__ __launch_bounds__(T, 4) void rl_decode_kernel(  // 2nd: waves per SIM
             c += (tid >> i) & 1;
             e |= (uint64_t)c << (8 * i);
         }
-        s_pfx[tid] = e;  // read after the first tile's barriers
+        s_pfx[pfx_slot(tid)] = e;  // read after the first tile's barriers
     }
     u32x4 cv = load16_tail(counts, tile * kRdRuns + tid * RPT, runs);
     u32x4 vv = load16_tail(values, tile * kRdRuns + tid * RPT, runs);
@@ -1558,7 +1567,7 @@ __global__ __launch_bounds__(kWdThreads) void rl_decode_wave_kernel(
     __shared__ u32x4 s_val4[NW][TR / 16 + 2];  // +32 B: the permute window reads up to 19 bytes past a run
     __shared__ u32x4 s_bm4[NW][kWdWords / 4 + 1];   // +1: a single-window tile's past-the-end marks
     __shared__ u32x4 s_pre4[NW][kWdWords / 4];      // starts in the window before word w
-    __shared__ uint64_t s_pfx[256];                 // byte i of s_pfx[x] = popcount(x & ((2 << i) - 1))
+    __shared__ uint64_t s_pfx[kPfxSlots];           // byte i of s_pfx[pfx_slot(x)] = popcount(x & ((2 << i) - 1))
     const int tid = threadIdx.x;
     const int lane = tid & (kWave - 1);
     const int wave = tid / kWave;
@@ -1571,7 +1580,7 @@ __global__ __launch_bounds__(kWdThreads) void rl_decode_wave_kernel(
             c += (tid >> i) & 1;
             e |= (uint64_t)c << (8 * i);
         }
-        s_pfx[tid] = e;
+        s_pfx[pfx_slot(tid)] = e;
     }
     __syncthreads();  // the only block barrier
     const uint64_t stride = (uint64_t)gridDim.x * NW;
