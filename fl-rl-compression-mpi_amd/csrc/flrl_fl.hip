@@ -25,8 +25,8 @@
 // Decode is two launches: fl_offsets_kernel scans the frame widths (F bytes,
 // <1% of the traffic) into per-tile output offsets and validates the widths
 // and valuesSize; fl_decode_kernel is then a streaming kernel with no
-// inter-workgroup dependency: persistent grid-stride workgroups take 32 KiB
-// output tiles, load each tile's widths and contiguous packed bytes (16-B
+// inter-workgroup dependency: persistent workgroups take 64 KiB output tiles
+// by ticket, load each tile's widths and contiguous packed bytes (16-B
 // aligned) one tile ahead into registers, stage the bytes in LDS and unpack
 // 2b bytes -> 16 bytes per lane.
 //
@@ -455,14 +455,21 @@ __global__ __launch_bounds__(kThreads) void fl_offsets_kernel(
 // Decode: persistent 512-thread workgroups (kDecPerCU per CU) take 64 KiB
 // output tiles by ticket; the packed bytes (and frame widths) of a workgroup's
 // next tile are loaded into registers right after the current tile's width
-// scan, while the current tile is unpacked from LDS. Lane group g = tid/8 owns
-// frames g*ITEMS .. +ITEMS-1 of the tile (its prefix is a register running sum
-// after one wave scan); lane tid%8 unpacks 16-byte chunk tid%8 of each.
-// Measured against one 32 KiB tile per workgroup (round-1/2 harness ubench_decode.hip):
-// -6 % at 1 GiB u8, -5 % lo4, -13 % at 16 GiB. Grid-stride tiles instead of
-// tickets were as good at 1 GiB but 10 % slower at 16 GiB (workgroups drift
-// apart in the address space); 32 KiB tiles by ticket saturate the ticket
-// atomic; contiguous per-workgroup tile ranges (which would let the offsets
+// scan, while the current tile is unpacked from LDS. Wave w owns frames
+// 64w .. 64w+63 of the tile: lane l loads frame 64w+l's width, one wave scan
+// gives every frame's offset, and item k of lane l (chunk l%8 of frame
+// 64w+8k+l/8) takes its frame's offset and width by lane shuffle, so store
+// instruction k writes 1 KiB contiguous. (The round-3 order, lane group l/8
+// owning 8 consecutive frames, wrote 8 lines 1 KiB apart per instruction: 1 GiB
+// lo4 +1.4 %, all-zero +3 %, 16 GiB u8 +0.3 %, u8 equal, scripts/ab_libs.py.)
+// 64 KiB tiles: 2 per ticket were 6.4 % slower at 1 GiB, 7.6 % at 16 GiB, 4 per
+// ticket 10 / 14 % (every workgroup's current tile then has the same parity:
+// the concurrent addresses cover half the HBM interleave), and grid-stride
+// tiles 20 % (1 GiB) / 24 % (16 GiB); the tile_base loads cost nothing
+// measurable (offsets computed as for all-width-8 input: equal). Measured
+// against one 32 KiB tile per workgroup (round-1/2 harness ubench_decode.hip):
+// -6 % at 1 GiB u8, -5 % lo4, -13 % at 16 GiB; 32 KiB tiles by ticket
+// saturate the ticket atomic; contiguous per-workgroup tile ranges (which would let the offsets
 // pre-pass fuse into this kernel) were 20 % slower.
 template <int ITEMS>
 __device__ __forceinline__ void dec_load_values(u32x4 (&a)[ITEMS], const uint8_t *values, uint64_t base,
@@ -483,16 +490,10 @@ __device__ __forceinline__ void dec_load_values(u32x4 (&a)[ITEMS], const uint8_t
     }
 }
 
-// The ITEMS (= 8) widths of lane group tid/8, bytes past nframes read as 0.
-__device__ __forceinline__ uint64_t dec_load_widths(const uint8_t *bits, uint64_t f0, uint64_t nframes)
+// The width of frame f (0 past nframes).
+__device__ __forceinline__ uint32_t dec_load_width1(const uint8_t *bits, uint64_t f, uint64_t nframes)
 {
-    if (f0 + 8 <= nframes)
-        return *reinterpret_cast<const uint64_t *>(bits + f0);
-    uint64_t v = 0;
-    uint8_t *p = reinterpret_cast<uint8_t *>(&v);
-    for (int i = 0; i < 8; ++i)
-        p[i] = f0 + i < nframes ? bits[f0 + i] : 0;
-    return v;
+    return f < nframes ? bits[f] : 0u;
 }
 
 template <int ITEMS>
@@ -501,7 +502,7 @@ __global__ __launch_bounds__(kDecThreads, kDecPerCU) void fl_decode_kernel(
     uint64_t vsize, uint8_t *__restrict__ out, uint64_t n, const uint64_t *__restrict__ tile_base,
     uint32_t ntiles, Ctrl *ctrl, uint32_t ticket0)
 {
-    static_assert(ITEMS == 8, "a lane group's widths are one u64");
+    static_assert(ITEMS * kWave / 8 == kWave, "a wave's 64 frames: 8 per item");
     constexpr int T = kDecThreads;
     constexpr int TB = T * 16 * ITEMS;
     constexpr int TF = TB / kFrame;
@@ -531,7 +532,7 @@ __global__ __launch_bounds__(kDecThreads, kDecPerCU) void fl_decode_kernel(
         return;
     u32x4 a[ITEMS];
     dec_load_values<ITEMS>(a, values, base, agg, vsize);
-    uint64_t wv = dec_load_widths(bits, (uint64_t)tile * TF + (tid >> 3) * ITEMS, nframes);
+    uint32_t wv = dec_load_width1(bits, (uint64_t)tile * TF + tid, nframes);
     for (;;) {
         if (tid == 0)  // read after the scan barrier below
             s_next[slot] = first_round ? tile + gridDim.x : atomicAdd(&ctrl->ticket, 1u) - ticket0;
@@ -543,18 +544,13 @@ __global__ __launch_bounds__(kDecThreads, kDecPerCU) void fl_decode_kernel(
         if (tid < 2)
             s_in[agg + tid] = u32x4{0u, 0u, 0u, 0u};
         // widths (clamped as fl_offsets_kernel clamps them; 0 past the last frame)
-        uint32_t bw[ITEMS];
-        uint32_t gtot = 0;
-#pragma unroll
-        for (int k = 0; k < ITEMS; ++k) {
-            const uint64_t f = (uint64_t)tile * TF + (tid >> 3) * ITEMS + k;
-            const uint32_t b = f < nframes ? clamp_width((uint32_t)(wv >> (8 * k)) & 0xFFu) : 0u;
-            bw[k] = b;
-            gtot += b;
-        }
-        const uint32_t gincl = wave_incl_scan_u32((lane & 7) == 0 ? gtot : 0u);
+        // lane l holds the width of frame 64 wave + l; item k of lane l is
+        // frame 64 wave + 8k + l/8: its offset and width come by lane shuffle
+        const uint32_t b1 = (uint64_t)tile * TF + tid < nframes ? clamp_width(wv) : 0u;
+        const uint32_t incl = wave_incl_scan_u32(b1);
         if (lane == kWave - 1)
-            s_wave[wave] = gincl;
+            s_wave[wave] = incl;
+        const uint32_t pk = ((incl - b1) << 4) | b1;
         __syncthreads();
         uint32_t wbase = 0;
 #pragma unroll
@@ -570,21 +566,20 @@ __global__ __launch_bounds__(kDecThreads, kDecPerCU) void fl_decode_kernel(
             base = tile_base[nxt];
             agg = (uint32_t)(tile_base[nxt + 1] - base);
             dec_load_values<ITEMS>(a, values, base, agg, vsize);
-            wv = dec_load_widths(bits, (uint64_t)nxt * TF + (tid >> 3) * ITEMS, nframes);
+            wv = dec_load_width1(bits, (uint64_t)nxt * TF + tid, nframes);
         }
 
         // ---- unpack 2b bytes -> 16 values per lane and item, store
         const uint32_t *s32 = reinterpret_cast<const uint32_t *>(s_in);
         const bool full = tile_off + TB <= n;
-        uint32_t run = wbase + gincl - gtot;  // widths before this group's first frame
-        uint8_t *dst = out + tile_off + (uint32_t)(tid >> 3) * ITEMS * kFrame + (tid & 7) * 16;
+        uint8_t *dst = out + tile_off + (uint32_t)wave * (kWave * kFrame) + lane * 16;
 #pragma unroll
         for (int k = 0; k < ITEMS; ++k) {
-            const uint32_t b = bw[k];
-            const uint32_t off = 16u * run + 2u * b * (uint32_t)(tid & 7);
-            run += b;
+            const uint32_t q = (uint32_t)__shfl((int)pk, 8 * k + (lane >> 3));
+            const uint32_t b = q & 0xFu;
             if (b == 0)
                 continue;
+            const uint32_t off = 16u * (wbase + (q >> 4)) + 2u * b * (uint32_t)(lane & 7);
             const uint32_t ad = off >> 2;
             const uint64_t w01 = ((uint64_t)s32[ad + 1] << 32) | s32[ad];
             const uint64_t w23 = ((uint64_t)s32[ad + 3] << 32) | s32[ad + 2];
@@ -599,10 +594,11 @@ __global__ __launch_bounds__(kDecThreads, kDecPerCU) void fl_decode_kernel(
             const uint64_t x1 = unpack8(p1, b);
             const u32x4 r = u32x4{(uint32_t)x0, (uint32_t)(x0 >> 32), (uint32_t)x1,
                                   (uint32_t)(x1 >> 32)};
+            constexpr uint32_t kStep = kWave * 16;  // item k: the wave's k-th KiB
             if (full)
-                __builtin_nontemporal_store(r, reinterpret_cast<u32x4 *>(dst + k * kFrame));
+                __builtin_nontemporal_store(r, reinterpret_cast<u32x4 *>(dst + k * kStep));
             else
-                store16_tail(out, (uint64_t)(dst - out) + k * kFrame, n, r);
+                store16_tail(out, (uint64_t)(dst - out) + k * kStep, n, r);
         }
         if (!more)
             break;

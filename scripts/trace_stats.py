@@ -37,3 +37,12 @@ w = lb - pub
 print("look-back wait share of tile time:", round(float(w.sum() / (end - start).sum()), 3))
 for k in range(i, i + 10):
     print(k, *(round(float(v), 2) for v in t[k]))
+# occupancy over the launch: tiles in flight per 10 us bin, and the share of
+# slot-time lost to the ramp-up and the tail (against the peak occupancy)
+peak = int(np.percentile(busy[busy > 0], 90))
+bins = [int(busy[k:k + 10].mean()) for k in range(0, len(busy), 10)]
+print("in flight per 10 us:", bins)
+span = float(end.max() - start.min())
+print("slot-time lost vs p90 occupancy", peak, ":", round(float(np.clip(peak - busy[:int(span)], 0, None).sum() / (peak * span)), 3))
+last = np.sort(start)[-peak:]
+print("last", peak, "tiles: started", round(float(last.min()), 1), "..", round(float(last.max()), 1), "us; kernel end", round(float(end.max()), 1))
