@@ -241,13 +241,15 @@ def north_star_section(seed: int, steps: int, warmup: int, dev):
     for _ in range(max(1, warmup)):
         codec.encode(x)
     v = codec.values_size()
-    ev = created_events(steps, 4, stream)  # call start/end, kernel start/end
+    ev = created_events(steps, 4, stream)  # call start/end, kernel start/end (separate passes)
     torch.cuda.synchronize()
     for k in range(steps):
         ev[k][0].record(stream)
-        flrl.time_next_kernel(ev[k][2], ev[k][3])
         codec.encode(x)
         ev[k][1].record(stream)
+    for k in range(steps):
+        flrl.time_next_kernel(ev[k][2], ev[k][3])
+        codec.encode(x)
     torch.cuda.synchronize()
     err = codec.error()
     enc_call_ms = mean_ms(ev, 0, 1)
@@ -262,9 +264,10 @@ def north_star_section(seed: int, steps: int, warmup: int, dev):
     (d0, d1, k0, k1), = created_events(1, 4, stream)
     codec.decode(v, out=out)
     d0.record(stream)
-    flrl.time_next_kernel(k0, k1)
     codec.decode(v, out=out)
     d1.record(stream)
+    flrl.time_next_kernel(k0, k1)
+    codec.decode(v, out=out)
     torch.cuda.synchronize()
     dec_call_ms = d0.elapsed_time(d1)
     dec_ms = k0.elapsed_time(k1)
@@ -273,7 +276,7 @@ def north_star_section(seed: int, steps: int, warmup: int, dev):
     res = {
         "workload": f"FL encode of {n} u8 bytes (seed {seed}) on 1 GPU (BASELINE north star)",
         "timing": "kernel time (HIP events around the kernel, flrl_time_next_kernel); call = + scratch "
-                  "zero-fill (decode: + offsets pre-pass)",
+                  "zero-fill (decode: + offsets pre-pass), timed in its own pass without the kernel events",
         "encode_ms": round(enc_ms, 4),
         "encode_median_ms": round(median_ms(ev, 2, 3), 4),
         "encode_call_ms": round(enc_call_ms, 4),
@@ -308,16 +311,21 @@ def _rl_timed(x, n: int, steps: int, warmup: int, dev):
     for _ in range(warmup):
         d.encode(x)
         d.decode(R)
-    ev = created_events(steps, 7, stream)  # calls: 0-1-2; kernels: 3-4 encode, 5-6 decode
+    # calls: events 0-1-2 (one pass); kernels alone: 3-4 encode, 5-6 decode (a
+    # second pass, so the call times hold no kernel-event records)
+    ev = created_events(steps, 7, stream)
     torch.cuda.synchronize()
     for k in range(steps):
         ev[k][0].record(stream)
-        flrl.time_next_kernel(ev[k][3], ev[k][4])
         d.encode(x)
         ev[k][1].record(stream)
-        flrl.time_next_kernel(ev[k][5], ev[k][6])
         d.decode(R)
         ev[k][2].record(stream)
+    for k in range(steps):
+        flrl.time_next_kernel(ev[k][3], ev[k][4])
+        d.encode(x)
+        flrl.time_next_kernel(ev[k][5], ev[k][6])
+        d.decode(R)
     torch.cuda.synchronize()
     if d.error():
         raise SystemExit(f"RL device error {d.error()} during the timed steps")
@@ -359,7 +367,8 @@ def rl_section(n: int, seed: int, steps: int, warmup: int, dev, cpu: bool):
         "value": round(n / ((enc_ms + dec_ms) * 1e-3) / 1e9, 2),
         "unit": "GB/s (input bytes, encode+decode)",
         "timing": f"median over {steps} encode/decode pairs after {warmup} warm-up pairs (HIP events); "
-                  "mean_ms = the mean of the same samples",
+                  "mean_ms = the mean of the same samples; call_ms from a separate pass of {steps} pairs "
+                  "without the kernel events".replace("{steps}", str(steps)),
         "rl_encode": {"ms": round(enc_k, 4), "mean_ms": round(enc_mean, 4), "call_ms": round(enc_ms, 4),
                       "alg_GBps": round(alg / (enc_k * 1e-3) / 1e9, 1),
                       "frac": round(alg / (enc_k * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
@@ -563,17 +572,24 @@ def main():
 
     # One step: encode (+ the exchange when scan: flrl_fl_encode_rank runs the
     # RCCL all-gather of {F_r, V_r} and the scan on the same stream), decode.
-    def step(e=None):
+    # Instrumented forms for the per-kernel breakdown: calls=True brackets the
+    # two device calls with events 0-1 / 2-3; calls=False brackets the two
+    # kernels alone with events 4-5 / 6-7 (flrl_time_next_kernel). Separate
+    # passes, so no call time holds the ~4.6 us of the kernel events' records.
+    def step(e=None, calls=True):
         if e is not None:
-            e[0].record(stream)
-            flrl.time_next_kernel(e[4], e[5])
+            if calls:
+                e[0].record(stream)
+            else:
+                flrl.time_next_kernel(e[4], e[5])
         encode()
-        if e is not None:
+        if e is not None and calls:
             e[1].record(stream)
             e[2].record(stream)
+        if e is not None and not calls:
             flrl.time_next_kernel(e[6], e[7])
         codec.decode(v, out=out)
-        if e is not None:
+        if e is not None and calls:
             e[3].record(stream)
 
     # ---- warmup ----
@@ -611,7 +627,9 @@ def main():
     ev = created_events(args.steps, 8, stream)
     torch.cuda.synchronize()
     for k in range(args.steps):
-        step(ev[k])
+        step(ev[k], calls=True)
+    for k in range(args.steps):
+        step(ev[k], calls=False)
     torch.cuda.synchronize()
     enc_call_ms = mean_ms(ev, 0, 1)  # + scratch zero-fill (+ the exchange when scan)
     dec_call_ms = mean_ms(ev, 2, 3)  # + zero-fill, offsets pre-pass
@@ -697,7 +715,8 @@ def main():
                 "timing": "ms / median_ms = mean / median over K steps of the kernel alone (HIP events "
                           "recorded by flrl_time_next_kernel on the launch stream); call_ms = the whole "
                           "device call (+ scratch zero-fill; + the size exchange when N > 1; decode: "
-                          "+ offsets pre-pass)",
+                          "+ offsets pre-pass), timed in a separate pass of K steps without the kernel "
+                          "events (each event record costs ~4.6 us of GPU timeline)",
                 "fl_encode": {"ms": round(enc_ms, 4), "median_ms": round(median_ms(ev, 4, 5), 4),
                               "call_ms": round(enc_call_ms, 4),
                               "alg_GBps": round(enc_gbs, 1),
