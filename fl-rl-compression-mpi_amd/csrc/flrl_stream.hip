@@ -445,10 +445,42 @@ struct SlotsLease {
 // chain of u64s, no writer thread): every pipeline writes its own bytes, so
 // host copies (memcpy or pwrite) run W-wide and a pipeline's buffers are never
 // read by another thread. *V_total = valuesSize.
+// FLRL_HOST_PROFILE (tuning builds): per-phase wall time of the compress
+// pipelines summed over workers, printed to stderr per call.
+#if FLRL_HOST_PROFILE
+static inline uint64_t prof_now()
+{
+    timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return (uint64_t)t.tv_sec * 1000000000ull + (uint64_t)t.tv_nsec;
+}
+struct HostProf {
+    std::atomic<uint64_t> ns[8];
+    const char *name[8] = {"read", "submit", "wait", "offsets", "write", "lease", "worker_wall", "thread_start"};
+    uint64_t t0 = prof_now();
+    HostProf() { for (auto &x : ns) x = 0; }
+    ~HostProf()
+    {
+        fprintf(stderr, "[host-prof] core_wall %.1f ms", (prof_now() - t0) * 1e-6);
+        for (int i = 0; i < 8; ++i)
+            fprintf(stderr, " %s %.1f ms", name[i], ns[i].load() * 1e-6);
+        fprintf(stderr, "\n");
+    }
+};
+#define PROF_T(v) const uint64_t v = prof_now()
+#define PROF_ADD(k, t0) prof.ns[k] += prof_now() - (t0)
+#else
+#define PROF_T(v) ((void)0)
+#define PROF_ADD(k, t0) ((void)0)
+#endif
+
 template <class Src, class Dst>
 int fl_compress_core(Src &src, Dst &dst, uint64_t n, const std::vector<int> &devs, int W, size_t chunk,
                      uint64_t *V_total, const char *who)
 {
+#if FLRL_HOST_PROFILE
+    HostProf prof;
+#endif
     const size_t cf = chunk / kFrame;
     const size_t nchunks = n ? (size_t)((n + chunk - 1) / chunk) : 0;
     *V_total = 0;
@@ -466,12 +498,23 @@ int fl_compress_core(Src &src, Dst &dst, uint64_t n, const std::vector<int> &dev
     const size_t scr_b = flrl_fl_scratch_bytes(chunk), vcap = flrl_fl_values_capacity(chunk);
 
     auto worker = [&](int w) {
+#if FLRL_HOST_PROFILE
+        const uint64_t tw0 = prof_now();
+        prof.ns[7] += tw0 - prof.t0;
+        struct WallEnd {
+            HostProf &p;
+            uint64_t t;
+            ~WallEnd() { p.ns[6] += prof_now() - t; }
+        } wall_end{prof, tw0};
+#endif
         const int dev = devs[(size_t)w % devs.size()];
         if (hipSetDevice(dev) != hipSuccess) {
             fail.set(FLRL_E_HIP, "hipSetDevice failed");
             return;
         }
+        PROF_T(tl);
         SlotsLease lease(dev, chunk, cf, vcap, scr_b);
+        PROF_ADD(5, tl);
         if (!lease.x) {
             fail.set(FLRL_E_NOMEM, "Cannot allocate memory (pinned staging)");
             return;
@@ -479,6 +522,7 @@ int fl_compress_core(Src &src, Dst &dst, uint64_t n, const std::vector<int> &dev
         Slots &S = *lease.x;
         auto finish = [&](size_t c, int k) -> bool {  // chunk c in slot k: check, place
             Slot &x = S.slot[k];
+            PROF_T(tw);
             if (hipStreamSynchronize(x.s) != hipSuccess) {
                 fail.set(FLRL_E_HIP, "fl encode: stream failed");
                 return false;
@@ -499,6 +543,8 @@ int fl_compress_core(Src &src, Dst &dst, uint64_t n, const std::vector<int> &dev
                 fail.set(FLRL_E_HIP, "fl encode: copy-out failed");
                 return false;
             }
+            PROF_ADD(2, tw);
+            PROF_T(to);
             uint64_t vo;
             {  // this chunk's values offset, then the next chunk's
                 std::unique_lock<std::mutex> g(m);
@@ -522,10 +568,13 @@ int fl_compress_core(Src &src, Dst &dst, uint64_t n, const std::vector<int> &dev
                 fail.set(FLRL_E_HIP, "fl encode: copy-out failed");
                 return false;
             }
+            PROF_ADD(3, to);
+            PROF_T(tr);
             if (!dst.write_bits(x.h_b, fb, (uint64_t)c * cf) || !dst.write_values(x.h_c, vb, vo)) {
                 fail.set(FLRL_E_ARG, "[FileIO] Cannot write to file");
                 return false;
             }
+            PROF_ADD(4, tr);
             return true;
         };
         size_t pend = SIZE_MAX;  // chunk in flight in slot pend_k
@@ -541,10 +590,13 @@ int fl_compress_core(Src &src, Dst &dst, uint64_t n, const std::vector<int> &dev
                 fail.set(FLRL_E_HIP, "injected failure (flrl_debug_fail_chunk)");
                 break;
             }
+            PROF_T(trd);
             if (!src.direct && !src.read(x.h_a, len, off)) {
                 fail.set(FLRL_E_ARG, "[FileIO] Cannot read file content");
                 break;
             }
+            PROF_ADD(0, trd);
+            PROF_T(ts);
             uint8_t *bits_to = dst.direct ? dst.bits_wptr((uint64_t)c * cf) : x.h_b;
             if (hipMemcpyAsync(x.d_a, src.direct ? src.ptr(off) : x.h_a, len, hipMemcpyHostToDevice, x.s) != hipSuccess ||
                 flrl_fl_encode_device(x.d_a, len, x.d_b, x.d_c, x.d_u64, x.d_scr, x.scr_bytes, x.s) != FLRL_OK ||
@@ -553,6 +605,7 @@ int fl_compress_core(Src &src, Dst &dst, uint64_t n, const std::vector<int> &dev
                 fail.set(FLRL_E_HIP, std::string("fl encode: ") + flrl_last_error());
                 break;
             }
+            PROF_ADD(1, ts);
             if (pend != SIZE_MAX && !finish(pend, pend_k))
                 break;
             pend = c;

@@ -16,7 +16,7 @@
      defined(FLRL_RL_STATUS_STRIDE) || defined(FLRL_RL_STATUS_OFF) ||\
      defined(FLRL_RL_STAGE) || defined(FLRL_RL_WPS) || defined(FLRL_RD_NARROW_MEAN) || defined(FLRL_RL_RO_MAXB) ||          \
      defined(FLRL_RD_UNROLL) || defined(FLRL_HOST_WORKERS) || defined(FLRL_HOST_CHUNK) ||                \
-     defined(FLRL_HOST_DIRECT) || defined(FLRL_HOST_THP) || defined(FLRL_RL_WD64_MEAN) || defined(FLRL_RL_DENSE_MEAN))
+     defined(FLRL_HOST_DIRECT) || defined(FLRL_HOST_PROFILE) || defined(FLRL_HOST_THP) || defined(FLRL_RL_WD64_MEAN) || defined(FLRL_RL_DENSE_MEAN))
 #error "FLRL_* kernel overrides are for timing harnesses only (define FLRL_TUNING_BUILD)"
 #endif
 
@@ -118,6 +118,9 @@
 #endif
 #ifndef FLRL_HOST_CHUNK
 #define FLRL_HOST_CHUNK (16ull << 20)
+#endif
+#ifndef FLRL_HOST_PROFILE
+#define FLRL_HOST_PROFILE 0
 #endif
 #ifndef FLRL_HOST_DIRECT
 #define FLRL_HOST_DIRECT 0

@@ -58,11 +58,6 @@ def mem_rates(n: int, kind: str, reps: int, ceiling: bool = True) -> dict:
     flrl._libc.free(ctypes.cast(b.bits, ctypes.c_void_p).value)
     flrl._libc.free(ctypes.cast(b.values, ctypes.c_void_p).value)
 
-    def comp_free():
-        b = comp()
-        flrl._libc.free(ctypes.cast(b.bits, ctypes.c_void_p).value)
-        flrl._libc.free(ctypes.cast(b.values, ctypes.c_void_p).value)
-
     def decomp():
         o, on = flrl._u8p(), ctypes.c_size_t(0)
         flrl._check(lib.flrl_fl_decompress(n, bits.ctypes.data, bits.size, vals.ctypes.data, vals.size,
@@ -74,14 +69,28 @@ def mem_rates(n: int, kind: str, reps: int, ceiling: bool = True) -> dict:
     res["roundtrip_ok"] = bool(np.array_equal(back, x))
     flrl._libc.free(ctypes.cast(o, ctypes.c_void_p).value)
 
-    def decomp_free():
-        flrl._libc.free(ctypes.cast(decomp(), ctypes.c_void_p).value)
-
-    tc, td = best(comp_free, reps), best(decomp_free, reps)
+    # The call alone (what the reference's [TIMER] brackets: main.cu times the
+    # gpuCompress / gpuDecompress call, the caller frees later) and the call
+    # plus the caller's free() of the outputs, best of `reps` each.
+    def split(call, outs):
+        tc_, tf_ = [], []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            r = call()
+            t1 = time.perf_counter()
+            for p in outs(r):
+                flrl._libc.free(ctypes.cast(p, ctypes.c_void_p).value)
+            tc_.append(t1 - t0)
+            tf_.append(time.perf_counter() - t0)
+        return min(tc_), min(tf_)
+    tc, tcf = split(comp, lambda b: (b.bits, b.values))
+    td, tdf = split(decomp, lambda o: (o,))
     res["compress_GBps"] = n / tc / 1e9
     res["decompress_GBps"] = n / td / 1e9
     res["compress_moved_GBps"] = (n + bits.size + vals.size) / tc / 1e9
     res["decompress_moved_GBps"] = (n + bits.size + vals.size) / td / 1e9
+    res["compress_with_free_GBps"] = n / tcf / 1e9
+    res["decompress_with_free_GBps"] = n / tdf / 1e9
     def first_touch():
         y = np.empty(n, dtype=np.uint8)  # fresh pages: what a malloc'd output costs
         y.fill(1)
@@ -102,6 +111,20 @@ def mem_rates(n: int, kind: str, reps: int, ceiling: bool = True) -> dict:
     res["pcie_d2h_pinned_GBps"] = n / best(cp(h, g), reps) / 1e9
     res["pcie_h2d_pageable_GBps"] = n / best(cp(g, p), reps) / 1e9
     res["host_memcpy_1thread_GBps"] = n / best(lambda: h.copy_(p), reps) / 1e9
+    # both directions at once (H2D on one stream, D2H on another; DMA copies):
+    # moved bytes per second, against twice the one-way rate if they overlap
+    h2 = torch.empty(n, dtype=torch.uint8, pin_memory=True)
+    g2 = torch.empty(n, dtype=torch.uint8, device="cuda")
+    sa, sb = torch.cuda.Stream(), torch.cuda.Stream()
+
+    def duplex():
+        with torch.cuda.stream(sa):
+            g.copy_(h, non_blocking=True)
+        with torch.cuda.stream(sb):
+            h2.copy_(g2, non_blocking=True)
+        torch.cuda.synchronize()
+    res["pcie_duplex_moved_GBps"] = 2 * n / best(duplex, reps) / 1e9
+
     return {k: (round(v, 3) if isinstance(v, float) else v) for k, v in res.items()}
 
 
