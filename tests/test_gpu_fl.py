@@ -91,7 +91,9 @@ def test_generated_golden(golden, idx):
 
 SIZES = [1, 2, 7, 8, 15, 16, 17, 127, 128, 129, 255, 256, 1000, 4096, 4741, 65535, 65536,
          65537, 100003, 131071, 131072, 131073, 196607, 196609, 262144 + 4095, 327744,
-         (1 << 20) + 13]  # decode tiles are 64 KiB, encode tiles 128 KiB
+         (1 << 20) + 13,
+         90769, 253951]  # decode tiles are 64 KiB (8 KiB of frames per wave), encode tiles 128 KiB;
+                         # the last two end inside a later wave of a decode tile
 
 
 @pytest.mark.parametrize("n", SIZES)
