@@ -537,12 +537,26 @@ __global__ __launch_bounds__(kDecThreads, kDecPerCU) void fl_decode_kernel(
         if (tid == 0)  // read after the scan barrier below
             s_next[slot] = first_round ? tile + gridDim.x : atomicAdd(&ctrl->ticket, 1u) - ticket0;
         first_round = false;
+        const uint64_t tile_off = (uint64_t)tile * TB;
+        // a whole tile whose 512 widths are all 8 (agg = 4096 units, the most
+        // its clamped widths can sum to) packs to itself: its bytes go straight
+        // from the load registers to the output, no LDS staging, no unpack
+        // (scripts/ab_libs.py: 1 GiB u8 -2.5 %, 256 MiB -3.1 %, 16 GiB -3.0 %;
+        // lo4 and all-zero, which never take it, equal)
+        const bool raw = agg == (uint32_t)(TB / 16) && tile_off + TB <= n;
+        if (raw) {
+            u32x4 *o = reinterpret_cast<u32x4 *>(out + tile_off) + tid;
 #pragma unroll
-        for (int k = 0; k < ITEMS; ++k)
-            if ((uint32_t)(k * T + tid) < agg)
-                s_in[k * T + tid] = a[k];
-        if (tid < 2)
-            s_in[agg + tid] = u32x4{0u, 0u, 0u, 0u};
+            for (int k = 0; k < ITEMS; ++k)
+                __builtin_nontemporal_store(a[k], o + k * T);
+        } else {
+#pragma unroll
+            for (int k = 0; k < ITEMS; ++k)
+                if ((uint32_t)(k * T + tid) < agg)
+                    s_in[k * T + tid] = a[k];
+            if (tid < 2)
+                s_in[agg + tid] = u32x4{0u, 0u, 0u, 0u};
+        }
         // widths (clamped as fl_offsets_kernel clamps them; 0 past the last frame)
         // lane l holds the width of frame 64 wave + l; item k of lane l is
         // frame 64 wave + 8k + l/8: its offset and width come by lane shuffle
@@ -561,7 +575,6 @@ __global__ __launch_bounds__(kDecThreads, kDecPerCU) void fl_decode_kernel(
         const uint32_t nxt = s_next[slot];
         slot ^= 1u;
         const bool more = nxt < ntiles;
-        const uint64_t tile_off = (uint64_t)tile * TB;
         if (more) {
             base = tile_base[nxt];
             agg = (uint32_t)(tile_base[nxt + 1] - base);
@@ -574,7 +587,7 @@ __global__ __launch_bounds__(kDecThreads, kDecPerCU) void fl_decode_kernel(
         const bool full = tile_off + TB <= n;
         uint8_t *dst = out + tile_off + (uint32_t)wave * (kWave * kFrame) + lane * 16;
 #pragma unroll
-        for (int k = 0; k < ITEMS; ++k) {
+        for (int k = 0; k < ITEMS && !raw; ++k) {
             const uint32_t q = (uint32_t)__shfl((int)pk, 8 * k + (lane >> 3));
             const uint32_t b = q & 0xFu;
             if (b == 0)

@@ -120,6 +120,30 @@ def test_every_width_in_one_tile():
     assert c.bits.tolist() == [1 + f % 8 for f in range(frames)]
 
 
+def test_raw_and_packed_decode_tiles():
+    # decode tiles (64 KiB) whose widths are all 8 are copied from the load
+    # registers; the others are unpacked through LDS. Alternate the two, with a
+    # width-7 frame at a tile's first, middle and last frame, then a partial
+    # last tile (never raw), through the host pipeline and the device API.
+    tile = 65536
+    n = 9 * tile + 5000
+    a = oracle.gen("u8", n, 21).copy()
+    for t, f in ((1, 0), (3, 255), (5, 511), (7, 100)):
+        o = t * tile + f * 128
+        a[o:o + 128] &= 0x7F
+    c = check_against_oracle(a)
+    assert [int(c.bits[t * 512:(t + 1) * 512].min()) for t in range(9)] == [8, 7, 8, 7, 8, 7, 8, 7, 8]
+    from flrl.device import FLDevice
+    x = torch.from_numpy(a).cuda()
+    d = FLDevice(n)
+    d.encode(x)
+    v = d.values_size()
+    assert v == c.values.size and d.error() == 0
+    d.decode(v)
+    assert d.error() == 0
+    assert torch.equal(d.out[:n], x)
+
+
 def test_many_tiles_random_widths():
     a = mixed_width_input(64 * 65536 + 777, 5)  # 65 tiles: look-back over > 64 tiles
     check_against_oracle(a)
