@@ -58,6 +58,8 @@ def main():
     kind = a.kind or ("runs32" if a.op.startswith("rl") else "u8")
     if kind in ("u8", "lo4", "zero"):
         x = gen(kind, n, 42)
+    elif kind in ("lo2", "lo1"):  # every FL frame of width 2 / 1 (and not all-zero)
+        x = gen("u8", n, 42) & (3 if kind == "lo2" else 1)
     elif kind.startswith("upto"):  # uniform run lengths 1..M (M = the number after "upto")
         import numpy as np
         rng = np.random.default_rng(42)
