@@ -500,7 +500,7 @@ template <int ITEMS>
 __global__ __launch_bounds__(kDecThreads, kDecPerCU) void fl_decode_kernel(
     const uint8_t *__restrict__ bits, uint64_t nframes, const uint8_t *__restrict__ values,
     uint64_t vsize, uint8_t *__restrict__ out, uint64_t n, const uint64_t *__restrict__ tile_base,
-    uint32_t ntiles, Ctrl *ctrl, uint32_t ticket0)
+    uint32_t ntiles, Ctrl *ctrl, uint32_t ticket0, uint32_t all8)
 {
     static_assert(ITEMS * kWave / 8 == kWave, "a wave's 64 frames: 8 per item");
     constexpr int T = kDecThreads;
@@ -517,6 +517,10 @@ __global__ __launch_bounds__(kDecThreads, kDecPerCU) void fl_decode_kernel(
     // -1 % more for the second); later tiles by ticket, numbered past them
     // (fl_offsets_kernel's workgroups took tickets 0..ticket0-1 of the same
     // counter): workgroups progress through the output in order
+    // a launch draws exactly ntiles - G tickets past ticket0 (each workgroup
+    // one that fails), so a larger one means the scratch's counter was not
+    // reset for this launch (with the pre-pass, that kernel flags it first)
+    const uint32_t stale = ticket0 + (ntiles - gridDim.x);
     ticket0 -= 2u * gridDim.x;
     bool first_round = true;  // the second tile is grid-stride too (-1 %: no burst of tickets at the start)
     uint32_t tile = blockIdx.x;
@@ -526,16 +530,40 @@ __global__ __launch_bounds__(kDecThreads, kDecPerCU) void fl_decode_kernel(
     // a pre-pass that raised (a stale ticket leaves tile_base unwritten) ends
     // the decode before any offset is used; loaded beside the first offsets
     const uint32_t err = __hip_atomic_load(&ctrl->error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    uint64_t base = tile_base[tile];
-    uint32_t agg = (uint32_t)(tile_base[tile + 1] - base);
+    // all8 (valuesSize == n, no pre-pass): every frame packs to itself, so tile
+    // t's bytes are bytes [t TB, min((t+1) TB, n)) of values; each width is
+    // checked below instead (8, or for the last frame any width whose packed
+    // size is its byte count)
+    auto offsets = [&](uint32_t t, uint64_t &b, uint32_t &g) {
+        if (all8) {
+            b = (uint64_t)t * (TB / 16);
+            const uint64_t left = (n - (uint64_t)t * TB + 15) / 16;
+            g = (uint32_t)(left < (uint64_t)(TB / 16) ? left : (uint64_t)(TB / 16));
+        } else {
+            b = tile_base[t];
+            g = (uint32_t)(tile_base[t + 1] - b);
+        }
+    };
+    uint64_t base;
+    uint32_t agg;
+    offsets(tile, base, agg);
     if (err != 0)
         return;
+    const uint64_t cnt_last = n - (nframes - 1) * kFrame;  // bytes in the last frame
     u32x4 a[ITEMS];
     dec_load_values<ITEMS>(a, values, base, agg, vsize);
     uint32_t wv = dec_load_width1(bits, (uint64_t)tile * TF + tid, nframes);
     for (;;) {
-        if (tid == 0)  // read after the scan barrier below
-            s_next[slot] = first_round ? tile + gridDim.x : atomicAdd(&ctrl->ticket, 1u) - ticket0;
+        if (tid == 0) {  // read after the scan barrier below
+            uint32_t nt = tile + gridDim.x;
+            if (!first_round) {
+                const uint32_t tk = atomicAdd(&ctrl->ticket, 1u);
+                if (tk >= stale)
+                    raise_error(ctrl, FLRL_E_ARG);
+                nt = tk - ticket0;
+            }
+            s_next[slot] = nt;
+        }
         first_round = false;
         const uint64_t tile_off = (uint64_t)tile * TB;
         // a whole tile whose 512 widths are all 8 (agg = 4096 units, the most
@@ -560,7 +588,11 @@ __global__ __launch_bounds__(kDecThreads, kDecPerCU) void fl_decode_kernel(
         // widths (clamped as fl_offsets_kernel clamps them; 0 past the last frame)
         // lane l holds the width of frame 64 wave + l; item k of lane l is
         // frame 64 wave + 8k + l/8: its offset and width come by lane shuffle
-        const uint32_t b1 = (uint64_t)tile * TF + tid < nframes ? clamp_width(wv) : 0u;
+        const uint64_t fw = (uint64_t)tile * TF + tid;
+        const uint32_t b1 = fw < nframes ? clamp_width(wv) : 0u;
+        if (all8 && fw < nframes &&
+            (fw + 1 < nframes ? wv != 8u : (wv < 1u || wv > 8u || (cnt_last * wv + 7) / 8 != cnt_last)))
+            raise_error(ctrl, FLRL_E_FORMAT);  // valuesSize == n does not match this width
         const uint32_t incl = wave_incl_scan_u32(b1);
         if (lane == kWave - 1)
             s_wave[wave] = incl;
@@ -576,8 +608,7 @@ __global__ __launch_bounds__(kDecThreads, kDecPerCU) void fl_decode_kernel(
         slot ^= 1u;
         const bool more = nxt < ntiles;
         if (more) {
-            base = tile_base[nxt];
-            agg = (uint32_t)(tile_base[nxt + 1] - base);
+            offsets(nxt, base, agg);
             dec_load_values<ITEMS>(a, values, base, agg, vsize);
             wv = dec_load_width1(bits, (uint64_t)nxt * TF + tid, nframes);
         }
@@ -720,16 +751,23 @@ extern "C" int flrl_fl_decode_device(const uint8_t *d_bits, size_t bits_size,
     uint64_t *status = reinterpret_cast<uint64_t *>(ctrl + 1);
     uint64_t *tile_base =
         reinterpret_cast<uint64_t *>(static_cast<uint8_t *>(d_scratch) + L.dec_zero);
-    hipLaunchKernelGGL(fl_offsets_kernel, dim3((uint32_t)L.off_blocks), dim3(kThreads), 0, s,
-                       d_bits, (uint64_t)bits_size, (uint64_t)values_size, (uint64_t)n, tile_base,
-                       (uint32_t)L.dec_tiles, (uint32_t)L.off_blocks, (uint32_t)L.off_iters, ctrl, status);
-    FLRL_HIP(hipGetLastError());
+    // valuesSize == n: every frame must have width 8 (the last one: a width
+    // whose packed size is its byte count), so the offsets are known without
+    // the pre-pass; fl_decode_kernel checks each width instead
+    const bool all8 = values_size == n;
+    if (!all8) {
+        hipLaunchKernelGGL(fl_offsets_kernel, dim3((uint32_t)L.off_blocks), dim3(kThreads), 0, s,
+                           d_bits, (uint64_t)bits_size, (uint64_t)values_size, (uint64_t)n, tile_base,
+                           (uint32_t)L.dec_tiles, (uint32_t)L.off_blocks, (uint32_t)L.off_iters, ctrl, status);
+        FLRL_HIP(hipGetLastError());
+    }
     const size_t dgrid = (size_t)kDecPerCU * (size_t)cu_count();
     kernel_timing_begin(s);
     hipLaunchKernelGGL(fl_decode_kernel<kDecItems>,
                        dim3((uint32_t)(L.dec_tiles < dgrid ? L.dec_tiles : dgrid)), dim3(kDecThreads), 0,
                        s, d_bits, (uint64_t)bits_size, d_values, (uint64_t)values_size, d_out,
-                       (uint64_t)n, tile_base, (uint32_t)L.dec_tiles, ctrl, (uint32_t)L.off_blocks);
+                       (uint64_t)n, tile_base, (uint32_t)L.dec_tiles, ctrl,
+                       (uint32_t)(all8 ? 0 : L.off_blocks), (uint32_t)all8);
     kernel_timing_end(s);
     FLRL_HIP(hipGetLastError());
     return FLRL_OK;

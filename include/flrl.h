@@ -244,7 +244,10 @@ int flrl_fl_encode_device(const uint8_t *d_in, size_t n, uint8_t *d_bits, uint8_
 
 /* Device decode: n output bytes from bits/values. The kernel flags
  * FLRL_E_FORMAT in the scratch area when a width is outside [1,8] or
- * values_size differs from the size the widths imply. */
+ * values_size differs from the size the widths imply; the output is then
+ * undefined. values_size == n (every frame stored at width 8, e.g.
+ * incompressible data) skips the offsets pre-pass: the decode kernel derives
+ * the offsets and checks each width itself. */
 int flrl_fl_decode_device(const uint8_t *d_bits, size_t bits_size, const uint8_t *d_values,
                           size_t values_size, uint8_t *d_out, size_t n, void *d_scratch,
                           size_t scratch_bytes, void *stream);

@@ -203,6 +203,57 @@ def test_device_bad_width_flag():
     assert d.error() == flrl.E_FORMAT
 
 
+def test_device_all8_decode_checks_widths():
+    # valuesSize == n: the decode takes every frame as width 8 without the
+    # offsets pre-pass and checks each width itself (the last frame: any width
+    # whose packed size is its byte count)
+    from flrl.device import FLDevice
+    for n, last in ((2344 * 128 + 1, 0), (2344 * 128 + 2, None)):
+        a = oracle.gen("u8", n, 4).copy()
+        a[-1] = 200  # a 2-byte last frame of width 8
+        if last is not None:
+            a[-1] = last  # a 1-byte last frame of value 0: width 1, 1 packed byte
+        x = torch.from_numpy(a).cuda()
+        d = FLDevice(n)
+        d.encode(x)
+        v = d.values_size()
+        assert v == n and d.error() == 0
+        bits, values = oracle.fl_compress(a)
+        assert np.array_equal(d.bits[:d.frames].cpu().numpy(), bits)
+        assert np.array_equal(d.values[:v].cpu().numpy(), values)
+        assert torch.equal(d.decode(v), x) and d.error() == 0
+        for f, w in ((1234, 7), (1234, 0), (1234, 9), (d.frames - 1, 9), (d.frames - 1, 0)) + \
+                (((d.frames - 1, 4),) if last is None else ()):
+            bad = d.bits.clone()
+            bad[f] = w
+            d.decode(v, bits=bad)
+            assert d.error() == flrl.E_FORMAT, (n, f, w)
+        d.decode(v)
+        assert d.error() == 0 and torch.equal(d.out[:n], x)
+
+
+@pytest.mark.parametrize("kind", ["lo4", "u8"])
+def test_stale_scratch_all8_decode(kind):
+    """Past 1024 decode tiles the decode takes tickets; without the offsets
+    pre-pass (u8: valuesSize == n) the decode itself flags a counter that was
+    not reset (FLRL_E_ARG) instead of leaving tiles undecoded."""
+    from flrl.device import FLDevice
+    n = (96 << 20) + 5
+    x = torch.from_numpy(oracle.gen(kind, n, 9)).cuda()
+    d = FLDevice(n)
+    d.encode(x)
+    v = d.values_size()
+    assert d.error() == 0 and (v == n) == (kind == "u8")
+    d.decode(v)
+    assert d.error() == 0 and torch.equal(d.out[:n], x)
+    flrl.debug_skip_scratch_resets(1)
+    d.decode(v)
+    assert d.error() == flrl.E_ARG
+    d.out.zero_()
+    d.decode(v)
+    assert d.error() == 0 and torch.equal(d.out[:n], x)
+
+
 @pytest.mark.parametrize("n", [5000, (8 << 20) + 5])
 def test_stale_scratch_raises(n):
     """A launch on scratch whose ticket was not reset (flrl_debug_skip_scratch_resets)
