@@ -276,7 +276,7 @@ def north_star_section(seed: int, steps: int, warmup: int, dev):
     res = {
         "workload": f"FL encode of {n} u8 bytes (seed {seed}) on 1 GPU (BASELINE north star)",
         "timing": "kernel time (HIP events around the kernel, flrl_time_next_kernel); call = + scratch "
-                  "zero-fill (decode: + offsets pre-pass), timed in its own pass without the kernel events",
+                  "zero-fill (decode: + the offsets pre-pass, skipped when valuesSize == n), timed in its own pass without the kernel events",
         "encode_ms": round(enc_ms, 4),
         "encode_median_ms": round(median_ms(ev, 2, 3), 4),
         "encode_call_ms": round(enc_call_ms, 4),
@@ -632,7 +632,7 @@ def main():
         step(ev[k], calls=False)
     torch.cuda.synchronize()
     enc_call_ms = mean_ms(ev, 0, 1)  # + scratch zero-fill (+ the exchange when scan)
-    dec_call_ms = mean_ms(ev, 2, 3)  # + zero-fill, offsets pre-pass
+    dec_call_ms = mean_ms(ev, 2, 3)  # + zero-fill, offsets pre-pass (none when valuesSize == n)
     enc_ms, dec_ms = mean_ms(ev, 4, 5), mean_ms(ev, 6, 7)  # the kernels alone
     if codec.error():
         raise SystemExit(f"device error {codec.error()} during the timed steps")
@@ -715,7 +715,7 @@ def main():
                 "timing": "ms / median_ms = mean / median over K steps of the kernel alone (HIP events "
                           "recorded by flrl_time_next_kernel on the launch stream); call_ms = the whole "
                           "device call (+ scratch zero-fill; + the size exchange when N > 1; decode: "
-                          "+ offsets pre-pass), timed in a separate pass of K steps without the kernel "
+                          "+ the offsets pre-pass unless valuesSize == n), timed in a separate pass of K steps without the kernel "
                           "events (each event record costs ~4.6 us of GPU timeline)",
                 "fl_encode": {"ms": round(enc_ms, 4), "median_ms": round(median_ms(ev, 4, 5), 4),
                               "call_ms": round(enc_call_ms, 4),
