@@ -103,6 +103,8 @@ def parse():
                    help="skip the configs[4] section (16 GiB per GPU through flrl_fl_encode_rank)")
     p.add_argument("--configs4-bytes", type=int, default=16 << 30,
                    help="bytes per GPU of the configs[4] section (runs at N>1, and at N=1 with --force-scan)")
+    p.add_argument("--no-configs3", action="store_true",
+                   help="skip the configs[3] section (16 GiB and 1 GiB lo4 FL encode + decode, N=1)")
     p.add_argument("--no-rl-dense", action="store_true",
                    help="skip the random-bytes RL section (profiles average kernels per name)")
     p.add_argument("--no-rl", action="store_true",
@@ -297,6 +299,75 @@ def north_star_section(seed: int, steps: int, warmup: int, dev):
     return res
 
 
+def fl_kind_timed(kind: str, n: int, seed: int, steps: int, warmup: int, dev) -> dict:
+    """FL encode and decode of n device-generated `kind` bytes on 1 GPU: the
+    kernels alone (HIP events by flrl_time_next_kernel) and the whole calls
+    (+ scratch zero-fill; decode + the offsets pre-pass, which runs unless
+    valuesSize == n) in separate passes, means over `steps`; frac on the
+    algorithmic bytes N + F + V; device round trip."""
+    x = gen(kind, n, seed, word_offset=0, device=dev)
+    codec = FLDevice(n, dev)
+    stream = torch.cuda.current_stream()
+    for _ in range(max(1, warmup)):
+        codec.encode(x)
+    v = codec.values_size()
+    out = torch.empty_like(x)
+    for _ in range(max(1, warmup)):
+        codec.decode(v, out=out)
+    ev = created_events(steps, 8, stream)
+    torch.cuda.synchronize()
+    for k in range(steps):
+        ev[k][0].record(stream)
+        codec.encode(x)
+        ev[k][1].record(stream)
+        codec.decode(v, out=out)
+        ev[k][2].record(stream)
+    for k in range(steps):
+        flrl.time_next_kernel(ev[k][4], ev[k][5])
+        codec.encode(x)
+        flrl.time_next_kernel(ev[k][6], ev[k][7])
+        codec.decode(v, out=out)
+    torch.cuda.synchronize()
+    ok = bool(torch.equal(out, x)) and codec.error() == 0
+    alg = n + codec.frames + v
+    enc_ms, dec_ms = mean_ms(ev, 4, 5), mean_ms(ev, 6, 7)
+    enc_call, dec_call = mean_ms(ev, 0, 1), mean_ms(ev, 1, 2)
+
+    def gbs(ms):
+        return alg / (ms * 1e-3) / 1e9
+    res = {
+        "bytes": n, "kind": kind, "values_size": v, "algorithmic_bytes_per_launch": alg,
+        "fl_encode": {"ms": round(enc_ms, 4), "call_ms": round(enc_call, 4), "alg_GBps": round(gbs(enc_ms), 1),
+                      "frac": round(gbs(enc_ms) / HBM_PEAK_GBS, 4),
+                      "traffic": pmc_traffic(kind, n, "fl_encode")},
+        "fl_decode": {"ms": round(dec_ms, 4), "call_ms": round(dec_call, 4), "alg_GBps": round(gbs(dec_ms), 1),
+                      "frac": round(gbs(dec_ms) / HBM_PEAK_GBS, 4),
+                      "call_frac": round(gbs(dec_call) / HBM_PEAK_GBS, 4),
+                      "traffic": pmc_traffic(kind, n, "fl_decode")},
+        "roundtrip": ok,
+    }
+    del x, out, codec
+    torch.cuda.empty_cache()
+    return res
+
+
+def configs3_section(seed: int, steps: int, warmup: int, dev) -> dict:
+    """BASELINE configs[3]: FL encode of 16 GiB low-entropy bytes (values
+    0-15: every frame at width 4, V = N/2) on 1 GPU against the HBM roofline,
+    with the decode of the same data (the general decode: offsets pre-pass +
+    LDS unpack, which the u8 headline never takes since valuesSize == n there),
+    and the same at 1 GiB. `traffic` = PMC HBM bytes per launch from
+    profiles/traffic_lo4_<bytes>.json when that summary exists."""
+    return {
+        "workload": "BASELINE configs[3]: FL encode (+ decode) of 17179869184 lo4 bytes (values 0-15, "
+                    f"splitmix64 seed {seed}) on 1 GPU; also 1 GiB",
+        "timing": "means over K launches; ms = the kernel alone (HIP events by flrl_time_next_kernel), "
+                  "call_ms = the whole device call in a separate pass (decode: + the offsets pre-pass)",
+        "16GiB": fl_kind_timed("lo4", 16 << 30, seed, steps, warmup, dev),
+        "1GiB": fl_kind_timed("lo4", 1 << 30, seed, steps, warmup, dev),
+    }
+
+
 def _rl_timed(x, n: int, steps: int, warmup: int, dev):
     """RL encode + decode of x (n bytes in HBM): R, the round trip, and the
     MEDIAN whole-call / kernel-alone times of both over `steps` encode/decode
@@ -414,7 +485,7 @@ def _all_gather_obj(obj, world: int) -> list:
 
 
 def configs4_section(comm, rank: int, world: int, seed: int, steps: int, warmup: int, dev,
-                     n: int = 16 << 30):
+                     n: int = 16 << 30, rccl: dict | None = None):
     """BASELINE configs[4]: FL encode of 16 GiB uniform-random bytes per GPU
     (128 GiB at N = 8), rank r holding global bytes [r*n, (r+1)*n), through
     flrl_fl_encode_rank (encode + the RCCL all-gather of {F_r, V_r} + device
@@ -486,7 +557,8 @@ def configs4_section(comm, rank: int, world: int, seed: int, steps: int, warmup:
         "workload": f"{'BASELINE configs[4]' if n == 16 << 30 else 'configs[4] path, custom size'}: FL encode "
                     f"of {n} u8 bytes per GPU x{world} = {n * world} bytes (seed {seed}), flrl_fl_encode_rank "
                     f"(encode + RCCL size exchange)",
-        "ranks_seen": world,
+        "ranks_seen": rccl["comm_count"] if rccl else world,
+        "rccl": rccl,
         "value": round(world * n / (wall / steps) / 1e9, 2),
         "unit": "GB/s (input bytes, whole job)",
         "ms_per_step": round(wall * 1e3 / steps, 4),
@@ -520,6 +592,17 @@ def main():
         comm = flrl.Comm.rank(world, uid[0], rank)
     elif scan:
         comm = flrl.Comm.rank(1, flrl.comm_unique_id(), 0)
+    # what RCCL itself saw: its rank count, and each rank's device + PCI bus id
+    rccl = None
+    if comm is not None:
+        info = _all_gather_obj(comm.rccl_info(), world)
+        rccl = {"comm_count": info[0]["count"],
+                "counts_agree": all(i["count"] == info[0]["count"] for i in info),
+                "user_ranks": [i["rank"] for i in info],
+                "devices": [i["device"] for i in info],
+                "pci_bus_ids": [i["pci_bus_id"] for i in info],
+                "distinct_gpus": len({i["pci_bus_id"] for i in info})}
+    ranks_seen = rccl["comm_count"] if rccl else world
 
     def barrier():
         if world > 1:
@@ -661,7 +744,7 @@ def main():
         if args.configs4_bytes <= 0 or args.configs4_bytes % 128:
             raise SystemExit("--configs4-bytes must be a positive multiple of 128")
         c4 = configs4_section(comm, rank, world, args.seed, args.steps, args.warmup, dev,
-                              n=args.configs4_bytes)
+                              n=args.configs4_bytes, rccl=rccl)
 
     if rank == 0:
         cpu = None
@@ -671,6 +754,9 @@ def main():
         ns = None
         if world == 1 and not args.no_north_star and not (n == 16 << 30 and args.kind == "u8"):
             ns = north_star_section(args.seed, args.steps, args.warmup, dev)
+        c3 = None
+        if world == 1 and not args.no_configs3:
+            c3 = configs3_section(args.seed, args.steps, args.warmup, dev)
         rl = None
         if world == 1 and not args.no_rl:
             rl = rl_section(n, args.seed, args.steps, args.warmup, dev, cpu=sample > 0)
@@ -697,7 +783,8 @@ def main():
                 "global_bytes": total,
                 "parallelism": (f"dp{world}: 128-aligned shards, RCCL size exchange (flrl_fl_encode_rank)"
                                 if world > 1 else "single GPU"),
-                "ranks_seen": world,
+                "ranks_seen": ranks_seen,
+                "rccl": rccl,
                 "values_size_per_gpu": v,
                 "ratio": round((alg - n + 24) / n, 6),
             },
@@ -732,6 +819,7 @@ def main():
             "parity": parity,
             "rl": rl,
             "north_star": ns,
+            "configs3": c3,
             "configs4": c4,
         }
         print(json.dumps(line), flush=True)

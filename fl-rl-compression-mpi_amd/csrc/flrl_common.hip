@@ -175,6 +175,24 @@ extern "C" int flrl_debug_fail_chunk(long long chunk)
     return FLRL_OK;
 }
 
+static thread_local int g_fail_rank_step = 0;
+
+bool flrl::debug_fail_rank_step(int step)
+{
+    if (g_fail_rank_step != step)
+        return false;
+    g_fail_rank_step = 0;
+    return true;
+}
+
+extern "C" int flrl_debug_fail_rank_step(int step)
+{
+    if (step < 0 || step > FLRL_DEBUG_RANK_READ_SUM)
+        return set_error(FLRL_E_ARG, "flrl_debug_fail_rank_step: step %d", step);
+    g_fail_rank_step = step;
+    return FLRL_OK;
+}
+
 // flrl_debug_lookback_help_us: the decoupled-fallback threshold of this
 // thread's look-back launches in s_memrealtime ticks (-1: each kernel's default)
 static thread_local int64_t g_help_ticks = -1;

@@ -38,6 +38,9 @@ hipError_t raise_error_async(void *scratch, int code, hipStream_t s);
 uint64_t lookback_help_ticks(uint64_t dflt);
 // flrl_debug_fail_chunk: true when the streamed file paths should fail chunk c.
 bool debug_fail_chunk(size_t c);
+// flrl_debug_fail_rank_step: true (once) when this thread's next per-rank call
+// should fail at `step` (FLRL_DEBUG_RANK_*).
+bool debug_fail_rank_step(int step);
 
 // Host-buffer FL through the pinned chunk pipelines (flrl_stream.hip).
 int fl_compress_host(const uint8_t *data, size_t size, flrl_fl_buf *out);

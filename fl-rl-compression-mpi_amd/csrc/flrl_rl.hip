@@ -429,18 +429,18 @@ __device__ __forceinline__ void wave_lds_sync()
 // prefix (split heads before its first natural head), staged runs and, past a
 // staging overflow, re-read sub-chunks: sparse ones through the staging area,
 // dense ones one lane row at a time (contiguous stores).
-template <int LB, int SUB, int W>
+template <int LB, int SUB, int W, int STG = kRlStageBytes>
 struct RlWave {
     static constexpr int CH = LB / 16;      // 16-byte chunks per lane
     static constexpr int WB = kWave * LB;   // sub-chunk bytes
     static constexpr int CB = WB * SUB;     // wave chunk bytes
     static constexpr int TBT = CB * W;      // tile bytes
-    static constexpr int SW = kRlStageBytes / W / 2;  // staged records per wave
+    static constexpr int SW = STG / W / 2;  // staged records per wave
     static constexpr int NJ = WB / 1024;    // 1 KiB wave-loads per sub-chunk
     static constexpr int RPL = 1024 / LB;   // image rows per wave-load
     static constexpr uint32_t kNone = 0xFFFFFFFFu;
     // LDS per workgroup: W images and the run staging
-    static constexpr int kLdsBytes = W * WB + kRlStageBytes;
+    static constexpr int kLdsBytes = W * WB + STG;
     static_assert(LB == 64, "one u64 head mask per lane (piece emission: 4 x 16 positions)");
     static_assert(TBT == kRlTileBytes, "tile geometry shared with the layout");
 
@@ -471,8 +471,15 @@ struct RlWave {
     uint64_t n;
     uint8_t *img, *stc, *stv;
     const uint8_t *my;
-    int lane;
+    int lane, wi;
     uint32_t row, o, sw, swz_c;
+
+    // this wave's staging slice of a W-wave staging area at `st` (STG bytes)
+    __device__ void stage_at(uint8_t *st)
+    {
+        stc = st + wi * 2 * SW;
+        stv = stc + SW;
+    }
 
     // swizzle of row r: its chunk c sits at position c ^ swz(r); 16 lanes of a
     // ds_read_b128 (rows r..r+15, one chunk each) then cover all 64 banks
@@ -481,10 +488,10 @@ struct RlWave {
     __device__ RlWave(const uint8_t *in_, uint64_t n_, uint8_t *lds, int w_) : in(in_), n(n_)
     {
         const int w = (int)uniform32((uint32_t)w_);
+        wi = w;
         lane = threadIdx.x & (kWave - 1);
         img = lds + w * WB;
-        stc = lds + W * WB + w * 2 * SW;
-        stv = stc + SW;
+        stage_at(lds + W * WB);
         row = (uint32_t)lane;
         o = row * LB;
         my = img + o;
@@ -1060,6 +1067,294 @@ __global__ __launch_bounds__(T, kRlWavesPerSimd) void rl_encode_wave_kernel(  //
     // it (its status words were stale too, so the output is not trusted)
     if (tid == 0 && atomicAdd(&ctrl->ticket, 1u) >= ntiles)
         raise_error(ctrl, FLRL_E_ARG);
+}
+
+// ---- persistent RL encode: a look-back wave one tile behind the scan --------
+// Bytes [A, A + cnt) of dst = src[s0 .. s0 + cnt) (src in LDS, 4-byte aligned,
+// readable 20 bytes past its end), by one wave: a 16-byte store per lane for
+// every aligned chunk inside the range, naturally aligned 1/2/4/8-byte pieces
+// for the two chunks it shares with its neighbours (written by their owners).
+__device__ __forceinline__ void lds_flush(uint8_t *__restrict__ dst, uint64_t A, uint32_t cnt, const uint8_t *src,
+                                          uint32_t s0, int lane)
+{
+    const uint32_t a = (uint32_t)(A & 15u);
+    const uint32_t span = a + cnt;
+    uint8_t *const base = dst + (A - a);
+    const uint32_t *const s32 = reinterpret_cast<const uint32_t *>(src);
+    for (uint32_t q = (uint32_t)lane; cnt && 16 * q < span; q += kWave) {
+        const int32_t o = (int32_t)(16 * q) - (int32_t)a + (int32_t)s0;  // src index of the chunk's byte 0
+        const int32_t d = o >> 2;  // arithmetic: floor
+        const uint32_t sh = (uint32_t)o & 3u;
+        uint32_t wd[5];
+#pragma unroll
+        for (int i = 0; i < 5; ++i)
+            wd[i] = d + i < 0 ? 0u : s32[d + i];
+        const u32x4 v = u32x4{__builtin_amdgcn_alignbyte(wd[1], wd[0], sh), __builtin_amdgcn_alignbyte(wd[2], wd[1], sh),
+                              __builtin_amdgcn_alignbyte(wd[3], wd[2], sh), __builtin_amdgcn_alignbyte(wd[4], wd[3], sh)};
+        const uint32_t lo = q == 0 ? a : 0u;
+        const uint32_t hi = span - 16 * q < 16 ? span - 16 * q : 16u;
+        if (lo == 0 && hi == 16)
+            *reinterpret_cast<u32x4 *>(base + 16 * q) = v;
+        else
+            store_chunk_part(base + 16 * q, v, lo, hi);
+    }
+}
+
+// Bytes [A, A + cnt) of dst = the byte x, as lds_flush stores them.
+__device__ __forceinline__ void byte_fill(uint8_t *__restrict__ dst, uint64_t A, uint32_t cnt, uint32_t x, int lane)
+{
+    const uint32_t a = (uint32_t)(A & 15u);
+    const uint32_t span = a + cnt;
+    uint8_t *const base = dst + (A - a);
+    const uint32_t x4 = (x & 0xFFu) * 0x01010101u;
+    const u32x4 v = u32x4{x4, x4, x4, x4};
+    for (uint32_t q = (uint32_t)lane; cnt && 16 * q < span; q += kWave) {
+        const uint32_t lo = q == 0 ? a : 0u;
+        const uint32_t hi = span - 16 * q < 16 ? span - 16 * q : 16u;
+        if (lo == 0 && hi == 16)
+            *reinterpret_cast<u32x4 *>(base + 16 * q) = v;
+        else
+            store_chunk_part(base + 16 * q, v, lo, hi);
+    }
+}
+
+// FLRL_RL_LAG_GUARD (timing harnesses only): the look-back wave's stores are
+// bounds-checked; a violation skips the store and raises 90 + site with the
+// tile in Ctrl::aux (a fault probe, never in a shipped build).
+#ifdef FLRL_RL_LAG_GUARD
+#define RL_LAG_GUARD(ok, site, ctrl, tile)                                                  \
+    if (!(ok)) {                                                                            \
+        if ((threadIdx.x & 63) == 0) {                                                      \
+            atomicCAS(&(ctrl)->error, 0u, 90u + (site));                                    \
+            (ctrl)->aux = ((uint64_t)(tile) << 8) | (site);                                 \
+        }                                                                                   \
+        continue;                                                                           \
+    }
+#else
+#define RL_LAG_GUARD(ok, site, ctrl, tile)
+#endif
+#ifndef FLRL_RL_LAG_INLINE
+#define RL_LAG_CALL __noinline__
+#else
+#define RL_LAG_CALL __forceinline__
+#endif
+
+// What the look-back wave needs of a data wave's chunk to emit it (LDS).
+struct RlChunkInfo {
+    uint32_t first;   // first natural head (chunk-relative; kNone: none)
+    uint32_t K;       // state-independent heads (all staged unless overflowed)
+    uint32_t rel_in;  // PhaseMap over the chunk
+    uint32_t v0;      // the chunk's first byte; bit 8: the staging overflowed
+    uint32_t nst, Kst, rel_st, pad;  // the rest of the Chunk (overflowed tiles)
+};
+constexpr uint32_t kRlOverflow = 0x100u;
+
+// Emission of a whole tile whose runs are all staged, by the look-back wave
+// alone, with the tile's state st (heads before it, chunk state at its start):
+// chunk by chunk its split heads (255, v0), the run of its first natural head
+// (count from the incoming state) and the staged runs, as 16-byte stores.
+template <class Wv, int W>
+__device__ void rl_emit_staged_tile(const uint8_t *__restrict__ in, uint64_t n, uint8_t *stg, const RlChunkInfo *info, const uint64_t *maps,
+                                    uint32_t tile, uint64_t st, uint8_t *__restrict__ counts,
+                                    uint8_t *__restrict__ values, uint64_t *__restrict__ runs_out, Ctrl *ctrl)
+{
+    const int lane = threadIdx.x & (kWave - 1);
+#pragma unroll 1
+    for (int v = 0; v < W; ++v) {
+        RL_LAG_GUARD(sm_h(st) <= n && (st & kSmKind) == kSmConst, 0, ctrl, tile)
+        const uint64_t off = (uint64_t)tile * Wv::TBT + (uint64_t)v * Wv::CB;
+        if (off >= n)
+            break;
+        const uint32_t len = n - off < (uint64_t)Wv::CB ? (uint32_t)(n - off) : (uint32_t)Wv::CB;
+        const uint32_t first = uniform32(info[v].first), K = uniform32(info[v].K);
+        const uint32_t rel_in = uniform32(info[v].rel_in), v0 = uniform32(info[v].v0) & 0xFFu;
+        const uint64_t h_in = sm_h(st);
+        const uint32_t c_in = sm_c(st);
+        const uint32_t pre = first != Wv::kNone ? first : len;
+        const uint32_t S = splits(c_in, pre);
+        // split heads h_in + j (j < S) end 255-byte pieces of v0; record g is
+        // output byte g - 1 (record 0, the input's first head, ends no run)
+        RL_LAG_GUARD(K <= Wv::SW && S <= 130 && h_in + S + K <= n, 1, ctrl, tile)
+        {
+            const uint64_t g = h_in == 0 ? 1 : h_in, e = h_in + S;
+            if (e > g) {
+                byte_fill(counts, g - 1, (uint32_t)(e - g), 255u, lane);
+                byte_fill(values, g - 1, (uint32_t)(e - g), v0, lane);
+            }
+        }
+        const uint64_t g0 = h_in + S;  // record of the first natural head
+        if (K) {
+            uint8_t *const sc = stg + v * 2 * Wv::SW;
+            uint8_t *const sv = sc + Wv::SW;
+            if (lane == 0) {
+                const uint32_t c = add_c(c_in, first);
+                sc[0] = (uint8_t)(c == 0 ? 255u : c);
+            }
+            wave_lds_sync();
+            const uint32_t j0 = g0 == 0 ? 1u : 0u;
+            lds_flush(counts, g0 + j0 - 1, K - j0, sc, j0, lane);
+            lds_flush(values, g0 + j0 - 1, K - j0, sv, j0, lane);
+        }
+        if (off + len == n && lane == 0) {  // the final run (ends at byte n-1)
+            const uint64_t R = g0 + K;
+            const uint32_t c_end = pm_apply(rel_in, c_in);
+            counts[R - 1] = (uint8_t)(c_end == 0 ? 255u : c_end);
+            values[R - 1] = in[n - 1];
+            *runs_out = R;
+        }
+        st = sm_compose(st, maps[v]);
+    }
+}
+
+// The look-back wave's part of a tile (persistent form): publish the tile's
+// map, resolve its state, then emit its staged runs -- or, when a chunk's
+// staging overflowed, hand the chunks' states to the data waves (s_st). Kept
+// out of line, as is the data waves' emission of overflowed tiles: inlined,
+// their registers added to the scan loop's and the kernel spilled.
+template <class Wv, int W>
+__device__ RL_LAG_CALL void rl_lag_resolve(const uint8_t *__restrict__ in, uint64_t n, uint8_t *stg, const RlChunkInfo *info, const uint64_t *maps,
+                                            uint64_t *s_st, bool ovf, uint32_t tile, uint8_t *__restrict__ counts,
+                                            uint8_t *__restrict__ values, uint64_t *__restrict__ runs_out,
+                                            Ctrl *ctrl, uint64_t *status, uint64_t help_ticks)
+{
+    uint64_t tmap = maps[0];
+#pragma unroll
+    for (int v = 1; v < W; ++v)
+        tmap = sm_compose(tmap, maps[v]);
+    publish_seg<kRlStatusStride>(status, tile, tmap);
+    FLRL_RL_TRACE(tile, 2);
+    auto help = [&](uint32_t t) -> uint64_t { return rl_tile_map_slow<Wv::TBT>(in, n, t); };
+    uint64_t st = lookback_seg<kRlLookG, kRlLookL, kRlStatusStride>(status, tile, tmap, ctrl, help_ticks, help);
+    FLRL_RL_TRACE(tile, 3);
+    if (ovf) {
+        if ((threadIdx.x & (kWave - 1)) == 0) {
+#pragma unroll
+            for (int v = 0; v < W; ++v) {
+                s_st[v] = st;
+                st = sm_compose(st, maps[v]);
+            }
+        }
+    } else {
+        rl_emit_staged_tile<Wv, W>(in, n, stg, info, maps, tile, st, counts, values, runs_out, ctrl);
+        FLRL_RL_TRACE(tile, 4);
+    }
+}
+
+// A data wave's emission of its chunk of an overflowed tile, the chunk's facts
+// read back from LDS (nothing of the scan stays live across the loop).
+template <class Wv>
+__device__ RL_LAG_CALL void rl_emit_overflowed(const uint8_t *__restrict__ in, uint64_t n, uint8_t *img, int w,
+                                                uint8_t *stg, const RlChunkInfo &I, uint32_t tile, uint64_t st,
+                                                uint8_t *__restrict__ counts, uint8_t *__restrict__ values,
+                                                uint64_t *__restrict__ runs_out)
+{
+    Wv V(in, n, img, w);
+    typename Wv::Chunk C;
+    C.off = uniform64((uint64_t)tile * Wv::TBT + (uint64_t)V.wi * Wv::CB);
+    C.len = C.off >= V.n ? 0u : (V.n - C.off < (uint64_t)Wv::CB ? (uint32_t)(V.n - C.off) : (uint32_t)Wv::CB);
+    C.ns = (int)((C.len + Wv::WB - 1) / Wv::WB);
+    C.nst = (int)uniform32(I.nst);
+    C.first = uniform32(I.first);
+    C.K = uniform32(I.K);
+    C.Kst = uniform32(I.Kst);
+    C.rel_in = uniform32(I.rel_in);
+    C.rel_st = uniform32(I.rel_st);
+    C.v0 = uniform32(I.v0) & 0xFFu;
+    V.stage_at(stg);
+    V.emit(C, sm_h(st), sm_c(st), counts, values, runs_out);
+}
+
+// Persistent form: one workgroup per slot (FLRL_RL_LAG_PER_CU per CU), W data
+// waves + one look-back wave. The data waves only scan: tile i's chunks into
+// staging buffer i mod 2, its maps and chunk facts to LDS, ONE barrier, then
+// straight on to tile i+1. Meanwhile the look-back wave publishes tile i,
+// resolves its state and emits its staged runs itself (16-byte stores), and
+// takes the ticket of tile i+2 -- so the data waves never wait for a
+// look-back unless it outlasts a whole tile scan. A tile whose staging
+// overflowed (dense runs: sub-chunks to re-read with the true states) is
+// emitted by its data waves as in rl_encode_wave_kernel, after a second
+// barrier at which the look-back wave hands over the states. The first tile of
+// a workgroup is its index, the rest by ticket (the ticket of the tile after
+// next is taken while this one is scanned, so its round trip is hidden).
+template <int T, int LB, int SUB, int STG>
+__global__ __launch_bounds__(T + kWave, FLRL_RL_LAG_WPS) void rl_encode_lag_kernel(
+    const uint8_t *__restrict__ in, uint64_t n, uint32_t ntiles, uint8_t *__restrict__ counts,
+    uint8_t *__restrict__ values, uint64_t *__restrict__ runs_out, Ctrl *ctrl, uint64_t *status,
+    uint64_t help_ticks)
+{
+    constexpr int W = T / kWave;
+    using Wv = RlWave<LB, SUB, W, STG>;
+    constexpr int kStg = STG + 32;  // + the flush's read slack
+    __shared__ __attribute__((aligned(16))) uint8_t s_img[W * Wv::WB];
+    __shared__ __attribute__((aligned(16))) uint8_t s_stg[2][kStg];
+    __shared__ uint64_t s_map[2][W];
+    __shared__ RlChunkInfo s_info[2][W];
+    __shared__ uint64_t s_st[W];
+    __shared__ uint32_t s_tile[2];
+
+    const int tid = threadIdx.x;
+    const int w = __builtin_amdgcn_readfirstlane(tid / kWave);
+    const bool lw = w == W;  // the look-back wave
+    Wv V(in, n, s_img, lw ? 0 : w);
+    uint32_t tile = blockIdx.x;
+    if (tile >= ntiles)
+        return;
+    // a tile ticket: tiles from gridDim.x on. A launch draws exactly ntiles
+    // tickets (each workgroup until its first past the end), so a raw ticket
+    // >= ntiles means the scratch's counter was not reset for this launch.
+    auto ticket = [&]() -> uint32_t {
+        const uint32_t raw = atomicAdd(&ctrl->ticket, 1u);
+        if (raw >= ntiles) {
+            raise_error(ctrl, FLRL_E_ARG);
+            return ntiles;
+        }
+        const uint64_t t = (uint64_t)raw + gridDim.x;
+        return t < ntiles ? (uint32_t)t : ntiles;
+    };
+    if (lw && V.lane == 0)
+        s_tile[1] = ticket();
+    auto scan = [&](uint32_t t, int b) {
+        V.stage_at(s_stg[b]);
+        const uint64_t off = (uint64_t)t * Wv::TBT + (uint64_t)w * Wv::CB;
+        typename Wv::Chunk C;
+        V.scan_chunk(off, off >= n ? 0u : (n - off < (uint64_t)Wv::CB ? (uint32_t)(n - off) : (uint32_t)Wv::CB), C);
+        if (V.lane == 0) {
+            s_map[b][w] = C.map();
+            s_info[b][w] = RlChunkInfo{C.first, C.K, C.rel_in, C.v0 | (C.nst < C.ns ? kRlOverflow : 0u),
+                                       (uint32_t)C.nst, C.Kst, C.rel_st, 0u};
+        }
+    };
+    FLRL_RL_TRACE(tile, 0);
+    if (!lw)
+        scan(tile, 0);
+    int b = 0;
+    for (;;) {
+        __syncthreads();  // tile scanned into staging b; s_tile[b ^ 1] = the next tile
+        FLRL_RL_TRACE(tile, 1);
+        const uint32_t nxt = s_tile[b ^ 1];
+        bool ovf = false;
+#pragma unroll
+        for (int v = 0; v < W; ++v)
+            ovf |= (s_info[b][v].v0 & kRlOverflow) != 0;
+        if (lw) {
+            // s_tile[b] was last read before the barrier above
+            if (nxt < ntiles && V.lane == 0)
+                s_tile[b] = ticket();
+            rl_lag_resolve<Wv, W>(in, n, s_stg[b], s_info[b], s_map[b], s_st, ovf, tile, counts, values, runs_out,
+                                  ctrl, status, help_ticks);
+        }
+        if (ovf) {
+            __syncthreads();  // the chunks' states in s_st
+            if (!lw)
+                rl_emit_overflowed<Wv>(in, n, s_img, w, s_stg[b], s_info[b][w], tile, s_st[w], counts, values, runs_out);
+        }
+        if (nxt >= ntiles)
+            break;
+        if (!lw)
+            scan(nxt, b ^ 1);
+        tile = nxt;
+        b ^= 1;
+    }
 }
 
 // ---- decode pre-pass: output offsets of each decode tile ------------------
@@ -1769,9 +2064,17 @@ extern "C" int flrl_rl_encode_device(const uint8_t *d_in, size_t n, uint8_t *d_c
     Ctrl *ctrl = static_cast<Ctrl *>(d_scratch);
     uint64_t *status = reinterpret_cast<uint64_t *>(static_cast<uint8_t *>(d_scratch) + kRlStatusOff);
     kernel_timing_begin(s);
-    hipLaunchKernelGGL((rl_encode_wave_kernel<kRlThreads, kRlLaneBytes, kRlSub>), dim3((uint32_t)L.tiles),
-                       dim3(kRlThreads), 0, s, d_in, (uint64_t)n, (uint32_t)L.tiles, d_counts, d_values,
-                       d_runs, ctrl, status, lookback_help_ticks(kRlHelpTicks));
+    if (FLRL_RL_LAG) {
+        const size_t slots = (size_t)FLRL_RL_LAG_PER_CU * (size_t)cu_count();
+        hipLaunchKernelGGL((rl_encode_lag_kernel<kRlThreads, kRlLaneBytes, kRlSub, FLRL_RL_LAG_STAGE>),
+                           dim3((uint32_t)(L.tiles < slots ? L.tiles : slots)), dim3(kRlThreads + kWave), 0, s, d_in,
+                           (uint64_t)n, (uint32_t)L.tiles, d_counts, d_values, d_runs, ctrl, status,
+                           lookback_help_ticks(kRlHelpTicks));
+    } else {
+        hipLaunchKernelGGL((rl_encode_wave_kernel<kRlThreads, kRlLaneBytes, kRlSub>), dim3((uint32_t)L.tiles),
+                           dim3(kRlThreads), 0, s, d_in, (uint64_t)n, (uint32_t)L.tiles, d_counts, d_values,
+                           d_runs, ctrl, status, lookback_help_ticks(kRlHelpTicks));
+    }
     kernel_timing_end(s);
     FLRL_HIP(hipGetLastError());
     return FLRL_OK;

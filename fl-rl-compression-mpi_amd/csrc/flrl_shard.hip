@@ -87,7 +87,12 @@ struct Dev {
     hipEvent_t cdone = nullptr;
     uint64_t *gather = nullptr;
     size_t gather_cap = 0;          // u64 entries
-    uint64_t *red = nullptr;        // 4 u64: flrl_fl_compress_rank's {size, failed} all-reduce
+    // 8 u64: [0, 4) flrl_fl_compress_rank's {size, failed} all-reduce (send,
+    // receive); [4, 8) constants written once at set-up: a failed exchange
+    // pair {failed word, 0} and a failed all-reduce word {0, 1}, the sources a
+    // rank that cannot stage its own words sends instead (no launch or copy
+    // needed on the failure path, so it still completes every collective)
+    uint64_t *red = nullptr;
     std::vector<hipEvent_t> ev;     // per local shard slot
 };
 
@@ -115,8 +120,18 @@ int dev_setup(Dev &d, size_t gather_entries)
         return set_error(FLRL_E_HIP, "hipStreamCreate failed on device %d", d.id);
     if (!d.cdone && hipEventCreateWithFlags(&d.cdone, hipEventDisableTiming) != hipSuccess)
         return set_error(FLRL_E_HIP, "hipEventCreate failed on device %d", d.id);
-    if (!d.red && hipMalloc(&d.red, 4 * sizeof(uint64_t)) != hipSuccess)
-        return set_error(FLRL_E_NOMEM, "Cannot allocate memory (device %d)", d.id);
+    if (!d.red) {
+        if (hipMalloc(&d.red, 8 * sizeof(uint64_t)) != hipSuccess) {
+            d.red = nullptr;
+            return set_error(FLRL_E_NOMEM, "Cannot allocate memory (device %d)", d.id);
+        }
+        const uint64_t k[8] = {0, 0, 0, 0, shard_failed_word(), 0, 0, 1};
+        if (hipMemcpy(d.red, k, sizeof(k), hipMemcpyHostToDevice) != hipSuccess) {
+            (void)hipFree(d.red);
+            d.red = nullptr;
+            return set_error(FLRL_E_HIP, "hipMemcpy failed on device %d", d.id);
+        }
+    }
     if (gather_entries > d.gather_cap) {
         if (d.gather) {  // the previous call's exchange may still read it
             (void)hipStreamSynchronize(d.cstream);
@@ -331,6 +346,34 @@ extern "C" int flrl_comm_query(const flrl_comm *c, int *nranks, int *rank, int *
     return FLRL_OK;
 }
 
+extern "C" int flrl_comm_rccl_info(const flrl_comm *c, int local, int *count, int *rank, int *device,
+                                   char *pci_bus_id, int len)
+{
+    if (!c || local < 0 || (size_t)local >= c->dev.size())
+        return set_error(FLRL_E_ARG, "flrl_comm_rccl_info: no local device %d", local);
+    const Dev &d = c->dev[(size_t)local];
+    int n = 0, r = 0, dv = -1;
+    ncclResult_t e = ncclCommCount(d.nccl, &n);
+    if (e == ncclSuccess)
+        e = ncclCommUserRank(d.nccl, &r);
+    if (e == ncclSuccess)
+        e = ncclCommCuDevice(d.nccl, &dv);
+    if (e != ncclSuccess)
+        return rccl_error(e, "flrl_comm_rccl_info");
+    if (count)
+        *count = n;
+    if (rank)
+        *rank = r;
+    if (device)
+        *device = dv;
+    if (pci_bus_id && len > 0) {
+        pci_bus_id[0] = 0;
+        if (hipDeviceGetPCIBusId(pci_bus_id, len, dv) != hipSuccess)
+            return set_error(FLRL_E_HIP, "hipDeviceGetPCIBusId(%d) failed", dv);
+    }
+    return FLRL_OK;
+}
+
 // ---- the exchange layout on the host (flrl_shard_layout.hpp) ---------------
 
 extern "C" int flrl_shard_range(size_t n, int nshards, int shard, size_t *start, size_t *length)
@@ -380,6 +423,10 @@ namespace {
 // encode does the same. Either way the all-gather runs on every rank, every
 // peer's scan raises FLRL_E_ARG, and this rank returns its own error; only a
 // comm that cannot take part at all (null, multi-device) returns before it.
+// A rank that cannot even reach its device or order its stream after the
+// previous call (a failed hipSetDevice / hipStreamWaitEvent) still sends: its
+// slot then comes from the comm's constant failed pair (Dev::red + 4), which
+// needs no launch (RCCL switches to the comm's device itself).
 int encode_rank_impl(flrl_comm *c, const uint8_t *d_in, size_t n, uint8_t *d_bits, uint8_t *d_values,
                      uint64_t *d_sizes, void *d_scratch, size_t scratch_bytes, void *stream, int local)
 {
@@ -397,15 +444,23 @@ int encode_rank_impl(flrl_comm *c, const uint8_t *d_in, size_t n, uint8_t *d_bit
         local = set_error(FLRL_E_ARG, "flrl_fl_encode_rank: current device %d, comm on device %d", prev, d.id);
     if (local == FLRL_OK && !d_sizes)
         local = set_error(FLRL_E_ARG, "flrl_fl_encode_rank: null sizes");
-    if (local != FLRL_OK) {  // the caller's stream may be unusable: the comm's own
+    bool staged = true;  // this rank can write its own slot
+    if (debug_fail_rank_step(FLRL_DEBUG_RANK_SET_DEVICE)) {
+        if (local == FLRL_OK)
+            local = set_error(FLRL_E_HIP, "flrl_fl_encode_rank: hipSetDevice(%d) failed (injected)", d.id);
         s = d.cstream;
-        if (hipSetDevice(d.id) != hipSuccess)
-            return local;
+        staged = false;
+    } else if (local != FLRL_OK) {  // the caller's stream may be unusable: the comm's own
+        s = d.cstream;
+        staged = hipSetDevice(d.id) == hipSuccess;
     }
     // the previous call's scan may still read the gather array on another stream
-    if (hipStreamWaitEvent(s, d.cdone, 0) != hipSuccess) {
-        (void)hipSetDevice(prev);
-        return local ? local : set_error(FLRL_E_HIP, "flrl_fl_encode_rank: event wait failed");
+    if (staged && (debug_fail_rank_step(FLRL_DEBUG_RANK_STREAM_WAIT) || hipStreamWaitEvent(s, d.cdone, 0) != hipSuccess)) {
+        if (local == FLRL_OK)
+            local = set_error(FLRL_E_HIP, "flrl_fl_encode_rank: event wait failed");
+        s = d.cstream;
+        // ordered on the host instead; failing that, send without touching the array
+        staged = hipEventSynchronize(d.cdone) == hipSuccess;
     }
     uint64_t *slot = d.gather + shard_slot((uint64_t)c->rank, (uint64_t)c->nranks, 1);
     if (local == FLRL_OK) {
@@ -417,10 +472,13 @@ int encode_rank_impl(flrl_comm *c, const uint8_t *d_in, size_t n, uint8_t *d_bit
         // on failure the failed pair follows the F word on the same stream (the
         // encode's argument checks precede every launch of it)
     }
-    if (local != FLRL_OK)
+    if (local != FLRL_OK && staged) {
         hipLaunchKernelGGL(put_pair_kernel, dim3(1), dim3(kWave), 0, s, slot, shard_failed_word(), (uint64_t)0);
-    const ncclResult_t r = ncclAllGather(slot, d.gather, 2, ncclUint64, d.nccl, s);  // in place
-    if (r != ncclSuccess) {
+        staged = hipGetLastError() == hipSuccess;
+    }
+    const ncclResult_t r = staged ? ncclAllGather(slot, d.gather, 2, ncclUint64, d.nccl, s)  // in place
+                                  : ncclAllGather(d.red + 4, d.gather, 2, ncclUint64, d.nccl, d.cstream);
+    if (r != ncclSuccess || !staged) {
         (void)hipSetDevice(prev);
         return local ? local : rccl_error(r, "ncclAllGather");
     }
@@ -790,38 +848,53 @@ extern "C" int flrl_fl_compress_rank(flrl_comm *c, const uint8_t *data, size_t s
         }
     }
     // (2) {whole input size (the reference all-gathers inputSize, fl_gpu.cu:105),
-    // ranks that failed}, summed over the ranks on the comm's own buffer/stream
-    uint64_t total_n = 0, failed = 0;
+    // ranks that failed}, summed over the ranks on the comm's own buffer/stream.
+    // The word is written by a kernel (its arguments travel with the launch, no
+    // pageable copy); a rank that cannot stage it sends the comm's constant
+    // {0, 1} instead (Dev::red + 6), so it is counted as failed either way.
+    uint64_t total_n = 0, failed = 1;
+    bool reduced = false;  // the all-reduce ran and its result was read back
     if (!rcl_broken) {
         std::lock_guard<std::mutex> g(c->mu);
         (void)hipSetDevice(dv.id);
-        const uint64_t mine[2] = {size, rc == FLRL_OK ? 0ull : 1ull};
-        uint64_t sum[2] = {0, 1};
-        ncclResult_t r1 = ncclSuccess;
-        if (hipStreamWaitEvent(dv.cstream, dv.cdone, 0) != hipSuccess ||
-            hipMemcpyAsync(dv.red, mine, sizeof(mine), hipMemcpyHostToDevice, dv.cstream) != hipSuccess) {
-            // cannot stage our word: still take part, with whatever the buffer
-            // holds, and count this rank as failed below
-            if (rc == FLRL_OK)
-                rc = set_error(FLRL_E_HIP, "flrl_fl_compress_rank: upload failed");
+        bool mine = !debug_fail_rank_step(FLRL_DEBUG_RANK_STAGE_WORD) &&
+                    hipStreamWaitEvent(dv.cstream, dv.cdone, 0) == hipSuccess;
+        if (mine) {
+            hipLaunchKernelGGL(put_pair_kernel, dim3(1), dim3(kWave), 0, dv.cstream, dv.red, (uint64_t)size,
+                               rc == FLRL_OK ? 0ull : 1ull);
+            mine = hipGetLastError() == hipSuccess;
         }
-        if ((r1 = ncclAllReduce(dv.red, dv.red + 2, 2, ncclUint64, ncclSum, dv.nccl, dv.cstream)) != ncclSuccess) {
+        if (!mine && rc == FLRL_OK)
+            rc = set_error(FLRL_E_HIP, "flrl_fl_compress_rank: staging {size, failed} failed");
+        uint64_t sum[2] = {0, 1};
+        const ncclResult_t r1 = ncclAllReduce(mine ? dv.red : dv.red + 6, dv.red + 2, 2, ncclUint64, ncclSum,
+                                              dv.nccl, dv.cstream);
+        if (r1 != ncclSuccess) {
             if (rc == FLRL_OK)
                 rc = rccl_error(r1, "ncclAllReduce");
-        } else if (hipMemcpyAsync(sum, dv.red + 2, sizeof(sum), hipMemcpyDeviceToHost, dv.cstream) != hipSuccess ||
+        } else if (debug_fail_rank_step(FLRL_DEBUG_RANK_READ_SUM) ||
+                   hipMemcpyAsync(sum, dv.red + 2, sizeof(sum), hipMemcpyDeviceToHost, dv.cstream) != hipSuccess ||
                    hipStreamSynchronize(dv.cstream) != hipSuccess) {
+            // the reduce completed on every rank, but this device cannot hand its
+            // result to the host: a device failure in the middle of the call. The
+            // peers decide (3) from the same sum; this rank cannot, so it leaves
+            // here -- if no rank had failed, the peers' (3) then fails or waits
+            // on this rank as any collective does on a dead device (RCCL).
             if (rc == FLRL_OK)
                 rc = set_error(FLRL_E_HIP, "flrl_fl_compress_rank: size read-back failed");
+        } else {
+            reduced = true;
         }
         total_n = sum[0];
         failed = sum[1];
-        if (rc == FLRL_OK && failed)
+        if (reduced && rc == FLRL_OK && failed)
             rc = set_error(FLRL_E_ARG, "flrl_fl_compress_rank: %llu rank(s) failed", (unsigned long long)failed);
     }
     // (3) the payloads to rank 0 (the reference's rank-0 merge, fl_gpu.cu:144-238,
-    // without padding or broadcasting them to every rank): only when every rank
-    // reported success in (2), so all ranks take this branch or none
-    if (rc == FLRL_OK && failed == 0 && !rcl_broken) {
+    // without padding or broadcasting them to every rank), gated on the
+    // all-reduced count alone: every rank that reads failed == 0 contributed 0,
+    // i.e. had succeeded so far, so all ranks take this branch or none
+    if (reduced && failed == 0 && !rcl_broken) {
         std::lock_guard<std::mutex> g(c->mu);
         ncclComm_t nc = dv.nccl;
         ncclResult_t r1 = ncclGroupStart();

@@ -16,7 +16,8 @@
      defined(FLRL_RL_STATUS_STRIDE) || defined(FLRL_RL_STATUS_OFF) ||\
      defined(FLRL_RL_STAGE) || defined(FLRL_RL_WPS) || defined(FLRL_RD_NARROW_MEAN) || defined(FLRL_RL_RO_MAXB) ||          \
      defined(FLRL_RD_UNROLL) || defined(FLRL_HOST_WORKERS) || defined(FLRL_HOST_CHUNK) ||                \
-     defined(FLRL_HOST_DIRECT) || defined(FLRL_HOST_PROFILE) || defined(FLRL_HOST_THP) || defined(FLRL_RL_WD64_MEAN) || defined(FLRL_RL_DENSE_MEAN))
+     defined(FLRL_HOST_DIRECT) || defined(FLRL_HOST_PROFILE) || defined(FLRL_HOST_THP) || defined(FLRL_RL_WD64_MEAN) || defined(FLRL_RL_DENSE_MEAN) ||\
+     defined(FLRL_RL_LAG) || defined(FLRL_RL_LAG_WPS) || defined(FLRL_RL_LAG_PER_CU) || defined(FLRL_RL_LAG_STAGE) || defined(FLRL_RL_LAG_GUARD) || defined(FLRL_RL_LAG_INLINE))
 #error "FLRL_* kernel overrides are for timing harnesses only (define FLRL_TUNING_BUILD)"
 #endif
 
@@ -81,6 +82,25 @@
 // 4-wave workgroups per CU, at most 96 VGPRs).
 #ifndef FLRL_RL_WPS
 #define FLRL_RL_WPS 5
+#endif
+
+// RL encode form: 1 = persistent workgroups with a look-back wave one tile
+// behind the scan (rl_encode_lag_kernel), 0 = one tile per workgroup
+// (rl_encode_wave_kernel).
+#ifndef FLRL_RL_LAG
+#define FLRL_RL_LAG 0
+#endif
+// persistent form: workgroups (4 data waves + the look-back wave) per CU, the
+// waves per SIMD they are compiled for, and each of the two staging buffers
+// (bytes per workgroup; 4 per CU leave 2 x 12032 beside the 16 KiB images)
+#ifndef FLRL_RL_LAG_PER_CU
+#define FLRL_RL_LAG_PER_CU 4
+#endif
+#ifndef FLRL_RL_LAG_WPS
+#define FLRL_RL_LAG_WPS 5
+#endif
+#ifndef FLRL_RL_LAG_STAGE
+#define FLRL_RL_LAG_STAGE 12032
 #endif
 
 // ---- RL decode shape ---------------------------------------------------------

@@ -116,6 +116,7 @@ _sig("flrl_time_next_kernel", ctypes.c_int, _vp, _vp)
 _sig("flrl_debug_skip_scratch_resets", ctypes.c_int, ctypes.c_int)
 _sig("flrl_debug_lookback_help_us", ctypes.c_int, ctypes.c_int)
 _sig("flrl_debug_fail_chunk", ctypes.c_int, ctypes.c_longlong)
+_sig("flrl_debug_fail_rank_step", ctypes.c_int, ctypes.c_int)
 _sig("flrl_rl_compress", ctypes.c_int, _vp, _sz, ctypes.POINTER(_RLBuf))
 _sig("flrl_rl_decompress", ctypes.c_int, _sz, _vp, _vp, _sz,
      ctypes.POINTER(_u8p), ctypes.POINTER(_sz))
@@ -133,6 +134,8 @@ _sig("flrl_comm_wrap", ctypes.c_int, _vp, _pp)
 _sig("flrl_comm_destroy", ctypes.c_int, _vp)
 _sig("flrl_comm_query", ctypes.c_int, _vp, ctypes.POINTER(ctypes.c_int),
      ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int))
+_sig("flrl_comm_rccl_info", ctypes.c_int, _vp, ctypes.c_int, ctypes.POINTER(ctypes.c_int),
+     ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int), ctypes.c_char_p, ctypes.c_int)
 _sig("flrl_fl_encode_rank", ctypes.c_int, _vp, _vp, _sz, _vp, _vp, _vp, _vp, _sz, _vp)
 _sig("flrl_fl_compress_rank", ctypes.c_int, _vp, _vp, _sz, ctypes.POINTER(_FLBuf))
 _sig("flrl_shard_range", ctypes.c_int, _sz, ctypes.c_int, ctypes.c_int, ctypes.POINTER(_sz),
@@ -314,6 +317,15 @@ class Comm:
         _check(_lib.flrl_comm_query(self.handle, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)))
         return a.value, b.value, c.value
 
+    def rccl_info(self, local: int = 0) -> dict:
+        """RCCL's own view of local device `local`: ncclCommCount, the user
+        rank, the HIP device and its PCI bus id (flrl_comm_rccl_info)."""
+        n, r, d = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        bus = ctypes.create_string_buffer(64)
+        _check(_lib.flrl_comm_rccl_info(self.handle, local, ctypes.byref(n), ctypes.byref(r), ctypes.byref(d),
+                                        bus, 64))
+        return {"count": n.value, "rank": r.value, "device": d.value, "pci_bus_id": bus.value.decode()}
+
     def encode_rank(self, d_in: int, n: int, d_bits: int, d_values: int, d_sizes: int,
                     d_scratch: int, scratch_bytes: int, stream: int = 0) -> None:
         _check(_lib.flrl_fl_encode_rank(self.handle, d_in, n, d_bits, d_values, d_sizes,
@@ -485,6 +497,15 @@ def debug_lookback_help_us(microseconds: int) -> None:
 def debug_fail_chunk(chunk: int) -> None:
     """Test hook: the streamed file paths fail at `chunk` (negative: never)."""
     _check(_lib.flrl_debug_fail_chunk(chunk))
+
+
+DEBUG_RANK_SET_DEVICE, DEBUG_RANK_STREAM_WAIT, DEBUG_RANK_STAGE_WORD, DEBUG_RANK_READ_SUM = 1, 2, 3, 4
+
+
+def debug_fail_rank_step(step: int) -> None:
+    """Test hook: this thread's next per-rank call fails once at `step`
+    (DEBUG_RANK_*; 0 cancels); see flrl_debug_fail_rank_step in include/flrl.h."""
+    _check(_lib.flrl_debug_fail_rank_step(step))
 
 
 def scratch_error(d_scratch: int, stream: int = 0) -> int:

@@ -137,6 +137,13 @@ int flrl_comm_init_rank(int nranks, const void *id, int rank, flrl_comm **out);
 int flrl_comm_wrap(void *nccl_comm, flrl_comm **out);
 int flrl_comm_destroy(flrl_comm *c);
 int flrl_comm_query(const flrl_comm *c, int *nranks, int *rank, int *ndev);
+/* What RCCL itself reports for the comm's local device `local` (0 for a
+ * per-rank comm): ncclCommCount, ncclCommUserRank, ncclCommCuDevice and that
+ * device's PCI bus id (hipDeviceGetPCIBusId, `len` bytes incl. the NUL) -- so a
+ * multi-GPU run can show that RCCL saw N ranks on N distinct GPUs. Any output
+ * pointer may be NULL. */
+int flrl_comm_rccl_info(const flrl_comm *c, int local, int *count, int *rank, int *device,
+                        char *pci_bus_id, int len);
 
 /* Per-rank device-resident encode + exchange (per-rank comm): encodes this
  * rank's shard like flrl_fl_encode_device, then fills d_sizes
@@ -285,6 +292,24 @@ int flrl_debug_lookback_help_us(int microseconds);
  * chunk (or RL decode block) `chunk`, as a failed read or device call would.
  * Process-wide; a negative value cancels. */
 int flrl_debug_fail_chunk(long long chunk);
+
+/* Test hook: the next flrl_fl_encode_rank / flrl_fl_compress_rank call of this
+ * thread fails once at `step`, as the runtime call there would, to exercise the
+ * collective-on-error paths (every rank still completes every collective):
+ *   FLRL_DEBUG_RANK_SET_DEVICE   the rank cannot reach its device: its exchange
+ *                                slot is sent from the comm's constant failed pair
+ *   FLRL_DEBUG_RANK_STREAM_WAIT  the stream cannot be ordered after the previous
+ *                                call: ordered on the host, failed slot
+ *   FLRL_DEBUG_RANK_STAGE_WORD   (compress_rank) the {size, failed} word cannot be
+ *                                staged: the constant {0, 1} is reduced instead
+ *   FLRL_DEBUG_RANK_READ_SUM     (compress_rank) the reduced word cannot be read
+ *                                back (a device failure after the all-reduce)
+ * 0 cancels. Never needed by callers. */
+#define FLRL_DEBUG_RANK_SET_DEVICE 1
+#define FLRL_DEBUG_RANK_STREAM_WAIT 2
+#define FLRL_DEBUG_RANK_STAGE_WORD 3
+#define FLRL_DEBUG_RANK_READ_SUM 4
+int flrl_debug_fail_rank_step(int step);
 
 /* ---- RL, host buffers (synchronous) --------------------------------------- */
 int flrl_rl_compress(const uint8_t *data, size_t size, flrl_rl_buf *out);

@@ -286,6 +286,56 @@ def test_encode_rank_local_error_still_exchanges(rank_comm):
     assert torch.equal(d.decode(v), x)
 
 
+@pytest.mark.parametrize("step", [flrl.DEBUG_RANK_SET_DEVICE, flrl.DEBUG_RANK_STREAM_WAIT])
+def test_encode_rank_runtime_failure_still_exchanges(rank_comm, step):
+    """a rank whose hipSetDevice or hipStreamWaitEvent
+    fails (injected, flrl_debug_fail_rank_step) still enters the all-gather --
+    from the comm's constant failed pair when it cannot reach its device, with
+    a failed slot written on the comm's stream otherwise -- so its peers never
+    wait in the collective. On a one-rank comm: the call returns FLRL_E_HIP,
+    and the comm keeps working."""
+    from flrl.device import FLDevice
+    n = 1 << 20
+    x = torch.randint(0, 256, (n,), dtype=torch.uint8, device="cuda")
+    d = FLDevice(n)
+    d.encode_rank(rank_comm, x)  # a successful call first: the slot holds a real record
+    torch.cuda.synchronize()
+    flrl.debug_fail_rank_step(step)
+    with pytest.raises(flrl.FLRLError) as e:
+        d.encode_rank(rank_comm, x)
+    assert e.value.code == flrl.E_HIP
+    torch.cuda.synchronize()
+    if step == flrl.DEBUG_RANK_STREAM_WAIT:  # the scan ran on the failed slot
+        assert [int(t) for t in d.rank_sizes[:flrl.SZ_COUNT].cpu()] == [0] * flrl.SZ_COUNT
+    d.encode_rank(rank_comm, x)  # the hook fired once; the next call works
+    torch.cuda.synchronize()
+    rec = [int(t) for t in d.rank_sizes[:flrl.SZ_COUNT].cpu()]
+    assert rec[flrl.SZ_F] == n // 128 and d.error() == 0
+    assert torch.equal(d.decode(rec[flrl.SZ_V]), x)
+
+
+@pytest.mark.parametrize("step", [flrl.DEBUG_RANK_SET_DEVICE, flrl.DEBUG_RANK_STREAM_WAIT,
+                                  flrl.DEBUG_RANK_STAGE_WORD, flrl.DEBUG_RANK_READ_SUM])
+def test_compress_rank_runtime_failure_returns(rank_comm, golden, bmp_bytes, step):
+    """flrl_fl_compress_rank with a failure injected at
+    each collective step -- the exchange (device unreachable, stream order),
+    staging the {size, failed} word (the constant {0, 1} is reduced instead),
+    reading the reduced word back -- returns an error instead of hanging, and
+    the next call on the same comm gives the reference result."""
+    flrl.debug_fail_rank_step(step)
+    with pytest.raises(flrl.FLRLError) as e:
+        rank_comm.compress_rank(bmp_bytes)
+    assert e.value.code == flrl.E_HIP
+    c = rank_comm.compress_rank(bmp_bytes)
+    assert file_sha(c.input_size, c.bits.tobytes(), c.values.tobytes()) == golden["fl_bmp"]["fl_sha256"]
+
+
+def test_debug_fail_rank_step_rejects_unknown():
+    with pytest.raises(flrl.FLRLError):
+        flrl.debug_fail_rank_step(9)
+    flrl.debug_fail_rank_step(0)
+
+
 def test_encode_rank_rejects_sharded_comm(local_comm):
     from flrl.device import FLDevice
     if flrl.device_count() > 1:
