@@ -1139,6 +1139,20 @@ __device__ __forceinline__ void byte_fill(uint8_t *__restrict__ dst, uint64_t A,
 #define RL_LAG_CALL __forceinline__
 #endif
 
+// Pointers into LDS and global memory that keep their address space across
+// the out-of-line calls below: passed as plain pointers, a callee sees generic
+// ones and every access becomes a flat instruction (LDS reads and global
+// stores alike); cast back to generic at the callee's top, the compiler infers
+// the space again and emits ds_ / global_ instructions.
+typedef __attribute__((address_space(3))) uint8_t lds_u8;
+typedef __attribute__((address_space(3))) uint64_t lds_u64;
+typedef __attribute__((address_space(1))) uint8_t glb_u8;
+typedef __attribute__((address_space(1))) uint64_t glb_u64;
+template <class T>
+__device__ __forceinline__ lds_u8 *as_lds(T *p) { return (lds_u8 *)(p); }
+__device__ __forceinline__ glb_u8 *as_glb(uint8_t *p) { return (glb_u8 *)(p); }
+__device__ __forceinline__ glb_u64 *as_glb(uint64_t *p) { return (glb_u64 *)(p); }
+
 // What the look-back wave needs of a data wave's chunk to emit it (LDS).
 struct RlChunkInfo {
     uint32_t first;   // first natural head (chunk-relative; kNone: none)
@@ -1212,11 +1226,21 @@ __device__ void rl_emit_staged_tile(const uint8_t *__restrict__ in, uint64_t n, 
 // out of line, as is the data waves' emission of overflowed tiles: inlined,
 // their registers added to the scan loop's and the kernel spilled.
 template <class Wv, int W>
-__device__ RL_LAG_CALL void rl_lag_resolve(const uint8_t *__restrict__ in, uint64_t n, uint8_t *stg, const RlChunkInfo *info, const uint64_t *maps,
-                                            uint64_t *s_st, bool ovf, uint32_t tile, uint8_t *__restrict__ counts,
-                                            uint8_t *__restrict__ values, uint64_t *__restrict__ runs_out,
-                                            Ctrl *ctrl, uint64_t *status, uint64_t help_ticks)
+__device__ RL_LAG_CALL void rl_lag_resolve(const glb_u8 *in_g, uint64_t n, lds_u8 *stg_l, lds_u8 *info_l,
+                                           lds_u8 *maps_l, lds_u8 *st_l, bool ovf, uint32_t tile,
+                                           glb_u8 *counts_g, glb_u8 *values_g, glb_u64 *runs_g, glb_u8 *ctrl_g,
+                                           glb_u64 *status_g, uint64_t help_ticks)
 {
+    const uint8_t *const in = (const uint8_t *)in_g;
+    uint8_t *const stg = (uint8_t *)stg_l;
+    const RlChunkInfo *const info = (const RlChunkInfo *)(uint8_t *)info_l;
+    const uint64_t *const maps = (const uint64_t *)(uint8_t *)maps_l;
+    uint64_t *const s_st = (uint64_t *)(uint8_t *)st_l;
+    uint8_t *const counts = (uint8_t *)counts_g;
+    uint8_t *const values = (uint8_t *)values_g;
+    uint64_t *const runs_out = (uint64_t *)runs_g;
+    Ctrl *const ctrl = (Ctrl *)(uint8_t *)ctrl_g;
+    uint64_t *const status = (uint64_t *)status_g;
     uint64_t tmap = maps[0];
 #pragma unroll
     for (int v = 1; v < W; ++v)
@@ -1243,12 +1267,17 @@ __device__ RL_LAG_CALL void rl_lag_resolve(const uint8_t *__restrict__ in, uint6
 // A data wave's emission of its chunk of an overflowed tile, the chunk's facts
 // read back from LDS (nothing of the scan stays live across the loop).
 template <class Wv>
-__device__ RL_LAG_CALL void rl_emit_overflowed(const uint8_t *__restrict__ in, uint64_t n, uint8_t *img, int w,
-                                                uint8_t *stg, const RlChunkInfo &I, uint32_t tile, uint64_t st,
-                                                uint8_t *__restrict__ counts, uint8_t *__restrict__ values,
-                                                uint64_t *__restrict__ runs_out)
+__device__ RL_LAG_CALL void rl_emit_overflowed(const glb_u8 *in_g, uint64_t n, lds_u8 *img_l, int w, lds_u8 *stg_l,
+                                               lds_u8 *info_l, uint32_t tile, uint64_t st, glb_u8 *counts_g,
+                                               glb_u8 *values_g, glb_u64 *runs_g)
 {
-    Wv V(in, n, img, w);
+    const uint8_t *const in = (const uint8_t *)in_g;
+    uint8_t *const stg = (uint8_t *)stg_l;
+    const RlChunkInfo &I = *(const RlChunkInfo *)(uint8_t *)info_l;
+    uint8_t *const counts = (uint8_t *)counts_g;
+    uint8_t *const values = (uint8_t *)values_g;
+    uint64_t *const runs_out = (uint64_t *)runs_g;
+    Wv V(in, n, (uint8_t *)img_l, w);
     typename Wv::Chunk C;
     C.off = uniform64((uint64_t)tile * Wv::TBT + (uint64_t)V.wi * Wv::CB);
     C.len = C.off >= V.n ? 0u : (V.n - C.off < (uint64_t)Wv::CB ? (uint32_t)(V.n - C.off) : (uint32_t)Wv::CB);
@@ -1340,13 +1369,15 @@ __global__ __launch_bounds__(T + kWave, FLRL_RL_LAG_WPS) void rl_encode_lag_kern
             // s_tile[b] was last read before the barrier above
             if (nxt < ntiles && V.lane == 0)
                 s_tile[b] = ticket();
-            rl_lag_resolve<Wv, W>(in, n, s_stg[b], s_info[b], s_map[b], s_st, ovf, tile, counts, values, runs_out,
-                                  ctrl, status, help_ticks);
+            rl_lag_resolve<Wv, W>((const glb_u8 *)in, n, as_lds(s_stg[b]), as_lds(s_info[b]), as_lds(s_map[b]),
+                                  as_lds(s_st), ovf, tile, as_glb(counts), as_glb(values), as_glb(runs_out),
+                                  (glb_u8 *)ctrl, as_glb(status), help_ticks);
         }
         if (ovf) {
             __syncthreads();  // the chunks' states in s_st
             if (!lw)
-                rl_emit_overflowed<Wv>(in, n, s_img, w, s_stg[b], s_info[b][w], tile, s_st[w], counts, values, runs_out);
+                rl_emit_overflowed<Wv>((const glb_u8 *)in, n, as_lds(s_img), w, as_lds(s_stg[b]), as_lds(&s_info[b][w]),
+                                       tile, s_st[w], as_glb(counts), as_glb(values), as_glb(runs_out));
         }
         if (nxt >= ntiles)
             break;

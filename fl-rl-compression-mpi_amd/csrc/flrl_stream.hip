@@ -31,6 +31,7 @@
 #include <sys/stat.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <atomic>
 #include <condition_variable>
 #include <list>
@@ -319,9 +320,16 @@ struct MemFl {  // FL arrays in host memory
 // frees every idle set. The host-buffer API's 8 pipelines of 16 MiB chunks
 // hold 8 x 2 x (16 MiB + 128 KiB + 16 MiB + 16) ~ 514 MiB of pinned memory per
 // direction (compress, decompress); the cap keeps both directions' sets (plus
-// slack), so alternating compress and decompress never reallocates.
+// slack), so alternating compress and decompress never reallocates. The file
+// APIs take workers and chunk sizes at run time, so the cap also grows to
+// twice the most pinned memory ever leased at once (both directions of the
+// largest call shape seen): more or larger pipelines than the host API's do
+// not re-allocate on every call either.
 constexpr size_t kHostSetBound = 2 * (2 * (size_t)FLRL_HOST_CHUNK + (size_t)FLRL_HOST_CHUNK / 128 + 16);
 constexpr size_t kPoolBytes = 2 * (size_t)FLRL_HOST_WORKERS * kHostSetBound + (64ull << 20);
+size_t g_leased_bytes = 0;       // pinned bytes of the sets leased right now
+size_t g_peak_leased_bytes = 0;  // the most ever leased at once
+size_t pool_cap() { return std::max(kPoolBytes, 2 * g_peak_leased_bytes + ((size_t)64 << 20)); }
 struct PoolKey {
     int dev;
     size_t a, b, c, scr;
@@ -358,6 +366,8 @@ Slots *slots_acquire(int dev, size_t a, size_t b, size_t c, size_t scr)
     const PoolKey k{dev, a, b, c, scr};
     {
         std::lock_guard<std::mutex> g(g_pool_m);
+        g_leased_bytes += k.pinned();  // (given back by slots_release, also for a failed lease)
+        g_peak_leased_bytes = std::max(g_peak_leased_bytes, g_leased_bytes);
         for (auto it = g_pool.rbegin(); it != g_pool.rend(); ++it)
             if (it->key == k) {
                 Slots *x = it->x;
@@ -385,6 +395,10 @@ Slots *slots_acquire(int dev, size_t a, size_t b, size_t c, size_t scr)
 
 void slots_release(Slots *x, size_t a, size_t b, size_t c, size_t scr)
 {
+    {
+        std::lock_guard<std::mutex> g(g_pool_m);
+        g_leased_bytes -= PoolKey{0, a, b, c, scr}.pinned();
+    }
     if (!x)
         return;
     for (Slot &y : x->slot)  // idle: nothing of a previous call still in flight
@@ -395,7 +409,7 @@ void slots_release(Slots *x, size_t a, size_t b, size_t c, size_t scr)
         const PoolKey k{x->dev, a, b, c, scr};
         g_pool.push_back(PoolEntry{k, x});
         g_pool_bytes += k.pinned();
-        while (g_pool_bytes > kPoolBytes && !g_pool.empty()) {
+        while (g_pool_bytes > pool_cap() && !g_pool.empty()) {
             g_pool_bytes -= g_pool.front().key.pinned();
             evict.push_back(g_pool.front().x);
             g_pool.pop_front();

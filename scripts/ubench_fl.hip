@@ -31,6 +31,13 @@ __device__ __forceinline__ uint64_t fl_rtime()
 #include "flrl_common.hip"
 #include "flrl_fl.hip"
 
+// the host-buffer pipelines live in flrl_stream.hip, which this harness does
+// not build: flrl_fl_compress / flrl_fl_decompress are never called here
+namespace flrl {
+int fl_compress_host(const uint8_t *, size_t, flrl_fl_buf *) { return FLRL_E_ARG; }
+int fl_decompress_host(size_t, const uint8_t *, size_t, const uint8_t *, size_t, uint8_t **) { return FLRL_E_ARG; }
+}  // namespace flrl
+
 #define CK(x)                                                                         \
     do {                                                                              \
         hipError_t e_ = (x);                                                          \

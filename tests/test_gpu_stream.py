@@ -412,6 +412,27 @@ def test_alternating_host_calls_keep_their_staging():
     assert freed >= 2 * 8 * 2 * (32 << 20), freed
 
 
+def test_alternating_file_calls_keep_larger_staging(tmp_path):
+    """the file APIs take workers and chunk sizes at run time; with
+    more pipelines or larger chunks than the host API's 8 x 16 MiB, the fixed
+    idle-pool cap evicted and re-allocated pinned sets on every alternating
+    compress/decompress call. The cap now grows to both directions of the
+    largest shape leased, so the idle pool keeps them all."""
+    import flrl
+    W, C = 12, 24 << 20
+    a = oracle.gen("lo4", W * C + 5, 23)
+    src, enc, back = tmp_path / "in", tmp_path / "enc", tmp_path / "back"
+    src.write_bytes(a.tobytes())
+    flrl.release_staging()
+    for _ in range(2):
+        flrl.fl_compress_file(str(src), str(enc), W, C)
+        flrl.fl_decompress_file(str(enc), str(back), W, C)
+    assert back.read_bytes() == a.tobytes()
+    freed = flrl.release_staging()
+    # both directions x W pipelines x 2 slots x (two C-byte buffers at least)
+    assert freed >= 2 * W * 2 * (2 * C), freed
+
+
 def test_release_staging_frees_idle_sets():
     """The host API keeps its pinned staging between calls (bounded); releasing
     it frees the idle sets, and the next call allocates afresh."""
