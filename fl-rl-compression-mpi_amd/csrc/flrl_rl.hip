@@ -51,6 +51,13 @@ constexpr int kRlThreads = FLRL_RL_THREADS;         // encode workgroup: 4 waves
 constexpr int kRlLaneBytes = 64;                    // contiguous bytes per lane (a u64 head mask)
 constexpr int kRlSub = 32768 / (64 * kRlLaneBytes); // sub-chunks per wave chunk (one look-back per tile)
 constexpr int kRlTileBytes = kRlLaneBytes * kRlThreads * kRlSub;  // 128 KiB: 4 waves x 32 KiB
+// persistent form (rl_encode_lag_kernel): FLRL_RL_LAG_WAVES data waves of 32 KiB
+// chunks + the look-back wave per workgroup
+constexpr int kRlLagWaves = FLRL_RL_LAG_WAVES;
+constexpr int kRlLagThreads = kWave * (kRlLagWaves + 1);
+constexpr int kRlLagTileBytes = kRlLaneBytes * kWave * kRlSub * kRlLagWaves;
+constexpr int kRlEncTileBytes = FLRL_RL_LAG ? kRlLagTileBytes : kRlTileBytes;  // tiles of the shipped form
+static_assert((uint64_t)kWave * FLRL_RL_LOOKG * kRlLagTileBytes < (1ull << 26), "look-back window maps within the 26-bit fields");
 constexpr int kRlLookG = FLRL_RL_LOOKG;  // look-back granules per lane (window 64 G tiles)
 constexpr int kRlLookL = FLRL_RL_LOOKL;  // look-back lanes polled per window
 constexpr int kRlStatusStride = FLRL_RL_STATUS_STRIDE;  // status granules per tile
@@ -397,6 +404,54 @@ __device__ __forceinline__ void store_chunk_part(uint8_t *dst, u32x4 v, uint32_t
         dst[a] = (uint8_t)(dw(a) >> (8 * (a & 3)));
 }
 
+// Bytes [A, A + cnt) of dst = src[s0 .. s0 + cnt) (src in LDS, 4-byte aligned,
+// readable 20 bytes past its end), by one wave: a 16-byte store per lane for
+// every aligned chunk inside the range, naturally aligned 1/2/4/8-byte pieces
+// for the two chunks it shares with its neighbours (written by their owners).
+__device__ __forceinline__ void lds_flush(uint8_t *__restrict__ dst, uint64_t A, uint32_t cnt, const uint8_t *src,
+                                          uint32_t s0, int lane)
+{
+    const uint32_t a = (uint32_t)(A & 15u);
+    const uint32_t span = a + cnt;
+    uint8_t *const base = dst + (A - a);
+    const uint32_t *const s32 = reinterpret_cast<const uint32_t *>(src);
+    for (uint32_t q = (uint32_t)lane; cnt && 16 * q < span; q += kWave) {
+        const int32_t o = (int32_t)(16 * q) - (int32_t)a + (int32_t)s0;  // src index of the chunk's byte 0
+        const int32_t d = o >> 2;  // arithmetic: floor
+        const uint32_t sh = (uint32_t)o & 3u;
+        uint32_t wd[5];
+#pragma unroll
+        for (int i = 0; i < 5; ++i)
+            wd[i] = d + i < 0 ? 0u : s32[d + i];
+        const u32x4 v = u32x4{__builtin_amdgcn_alignbyte(wd[1], wd[0], sh), __builtin_amdgcn_alignbyte(wd[2], wd[1], sh),
+                              __builtin_amdgcn_alignbyte(wd[3], wd[2], sh), __builtin_amdgcn_alignbyte(wd[4], wd[3], sh)};
+        const uint32_t lo = q == 0 ? a : 0u;
+        const uint32_t hi = span - 16 * q < 16 ? span - 16 * q : 16u;
+        if (lo == 0 && hi == 16)
+            *reinterpret_cast<u32x4 *>(base + 16 * q) = v;
+        else
+            store_chunk_part(base + 16 * q, v, lo, hi);
+    }
+}
+
+// Bytes [A, A + cnt) of dst = the byte x, as lds_flush stores them.
+__device__ __forceinline__ void byte_fill(uint8_t *__restrict__ dst, uint64_t A, uint32_t cnt, uint32_t x, int lane)
+{
+    const uint32_t a = (uint32_t)(A & 15u);
+    const uint32_t span = a + cnt;
+    uint8_t *const base = dst + (A - a);
+    const uint32_t x4 = (x & 0xFFu) * 0x01010101u;
+    const u32x4 v = u32x4{x4, x4, x4, x4};
+    for (uint32_t q = (uint32_t)lane; cnt && 16 * q < span; q += kWave) {
+        const uint32_t lo = q == 0 ? a : 0u;
+        const uint32_t hi = span - 16 * q < 16 ? span - 16 * q : 16u;
+        if (lo == 0 && hi == 16)
+            *reinterpret_cast<u32x4 *>(base + 16 * q) = v;
+        else
+            store_chunk_part(base + 16 * q, v, lo, hi);
+    }
+}
+
 // Wave-uniform values held in scalar registers (the compiler cannot prove
 // that values read from LDS or derived from the wave index are uniform).
 __device__ __forceinline__ uint32_t uniform32(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
@@ -429,7 +484,7 @@ __device__ __forceinline__ void wave_lds_sync()
 // prefix (split heads before its first natural head), staged runs and, past a
 // staging overflow, re-read sub-chunks: sparse ones through the staging area,
 // dense ones one lane row at a time (contiguous stores).
-template <int LB, int SUB, int W, int STG = kRlStageBytes>
+template <int LB, int SUB, int W, int STG = kRlStageBytes, int PFD = FLRL_RL_PF>
 struct RlWave {
     static constexpr int CH = LB / 16;      // 16-byte chunks per lane
     static constexpr int WB = kWave * LB;   // sub-chunk bytes
@@ -442,7 +497,7 @@ struct RlWave {
     // LDS per workgroup: W images and the run staging
     static constexpr int kLdsBytes = W * WB + STG;
     static_assert(LB == 64, "one u64 head mask per lane (piece emission: 4 x 16 positions)");
-    static_assert(TBT == kRlTileBytes, "tile geometry shared with the layout");
+    static_assert(TBT == kRlTileBytes || TBT == kRlLagTileBytes, "tile geometry shared with the layout");
 
     struct Sub {
         uint32_t nat[CH / 2];  // 16-bit natural-head masks, two per word
@@ -479,6 +534,23 @@ struct RlWave {
     {
         stc = st + wi * 2 * SW;
         stv = stc + SW;
+    }
+
+    // The lane-derived members again, from a lane index the compiler cannot
+    // see through: called at the top of each tile of a persistent loop, it
+    // keeps the per-lane addresses derived from them inside the iteration
+    // (hoisted out of the loop, they stayed live across it and the loop
+    // spilled).
+    __device__ void relane()
+    {
+        int l = (int)(threadIdx.x & (kWave - 1));
+        asm volatile("" : "+v"(l));
+        lane = l;
+        row = (uint32_t)l;
+        o = row * LB;
+        my = img + o;
+        sw = swz(row);
+        swz_c = ((uint32_t)l % CH) ^ swz((uint32_t)l / CH);
     }
 
     // swizzle of row r: its chunk c sits at position c ^ swz(r); 16 lanes of a
@@ -739,15 +811,17 @@ struct RlWave {
         C.len = len;
         C.ns = (int)((len + WB - 1) / WB);
         // PF sub-chunks in flight per wave (register sets used in turn)
-        constexpr int PF = FLRL_RL_PF;
-        static_assert(PF == 1 || PF == 2, "prefetch depth");
+        constexpr int PF = PFD;
+        static_assert(PF >= 1 && PF <= SUB && SUB % PF == 0, "prefetch depth");
         u32x4 pf[PF][NJ];
         uint32_t p_sub = 0;
         C.v0 = 0;
         if (C.ns > 0) {
             load_sub(off, 0, pf[0]);
-            if (PF == 2 && C.ns > 1)
-                load_sub(off, 1, pf[PF - 1]);
+#pragma unroll
+            for (int k = 1; k < PF; ++k)
+                if (k < C.ns)
+                    load_sub(off, k, pf[k]);
             p_sub = off > 0 ? (uint32_t)in[off - 1] : 0u;
         }
         uint32_t rel_in = kMapIdent;  // PhaseMap from the chunk start to this sub-chunk
@@ -794,8 +868,10 @@ struct RlWave {
         };
         for (int s = 0; s < C.ns; s += PF) {
             step(s, pf[0]);
-            if (PF == 2 && s + 1 < C.ns)
-                step(s + 1, pf[PF - 1]);
+#pragma unroll
+            for (int k = 1; k < PF; ++k)
+                if (s + k < C.ns)
+                    step(s + k, pf[k]);
         }
         if (nst >= C.ns) {
             nst = C.ns;
@@ -1070,54 +1146,6 @@ __global__ __launch_bounds__(T, kRlWavesPerSimd) void rl_encode_wave_kernel(  //
 }
 
 // ---- persistent RL encode: a look-back wave one tile behind the scan --------
-// Bytes [A, A + cnt) of dst = src[s0 .. s0 + cnt) (src in LDS, 4-byte aligned,
-// readable 20 bytes past its end), by one wave: a 16-byte store per lane for
-// every aligned chunk inside the range, naturally aligned 1/2/4/8-byte pieces
-// for the two chunks it shares with its neighbours (written by their owners).
-__device__ __forceinline__ void lds_flush(uint8_t *__restrict__ dst, uint64_t A, uint32_t cnt, const uint8_t *src,
-                                          uint32_t s0, int lane)
-{
-    const uint32_t a = (uint32_t)(A & 15u);
-    const uint32_t span = a + cnt;
-    uint8_t *const base = dst + (A - a);
-    const uint32_t *const s32 = reinterpret_cast<const uint32_t *>(src);
-    for (uint32_t q = (uint32_t)lane; cnt && 16 * q < span; q += kWave) {
-        const int32_t o = (int32_t)(16 * q) - (int32_t)a + (int32_t)s0;  // src index of the chunk's byte 0
-        const int32_t d = o >> 2;  // arithmetic: floor
-        const uint32_t sh = (uint32_t)o & 3u;
-        uint32_t wd[5];
-#pragma unroll
-        for (int i = 0; i < 5; ++i)
-            wd[i] = d + i < 0 ? 0u : s32[d + i];
-        const u32x4 v = u32x4{__builtin_amdgcn_alignbyte(wd[1], wd[0], sh), __builtin_amdgcn_alignbyte(wd[2], wd[1], sh),
-                              __builtin_amdgcn_alignbyte(wd[3], wd[2], sh), __builtin_amdgcn_alignbyte(wd[4], wd[3], sh)};
-        const uint32_t lo = q == 0 ? a : 0u;
-        const uint32_t hi = span - 16 * q < 16 ? span - 16 * q : 16u;
-        if (lo == 0 && hi == 16)
-            *reinterpret_cast<u32x4 *>(base + 16 * q) = v;
-        else
-            store_chunk_part(base + 16 * q, v, lo, hi);
-    }
-}
-
-// Bytes [A, A + cnt) of dst = the byte x, as lds_flush stores them.
-__device__ __forceinline__ void byte_fill(uint8_t *__restrict__ dst, uint64_t A, uint32_t cnt, uint32_t x, int lane)
-{
-    const uint32_t a = (uint32_t)(A & 15u);
-    const uint32_t span = a + cnt;
-    uint8_t *const base = dst + (A - a);
-    const uint32_t x4 = (x & 0xFFu) * 0x01010101u;
-    const u32x4 v = u32x4{x4, x4, x4, x4};
-    for (uint32_t q = (uint32_t)lane; cnt && 16 * q < span; q += kWave) {
-        const uint32_t lo = q == 0 ? a : 0u;
-        const uint32_t hi = span - 16 * q < 16 ? span - 16 * q : 16u;
-        if (lo == 0 && hi == 16)
-            *reinterpret_cast<u32x4 *>(base + 16 * q) = v;
-        else
-            store_chunk_part(base + 16 * q, v, lo, hi);
-    }
-}
-
 // FLRL_RL_LAG_GUARD (timing harnesses only): the look-back wave's stores are
 // bounds-checked; a violation skips the store and raises 90 + site with the
 // tile in Ctrl::aux (a fault probe, never in a shipped build).
@@ -1133,17 +1161,12 @@ __device__ __forceinline__ void byte_fill(uint8_t *__restrict__ dst, uint64_t A,
 #else
 #define RL_LAG_GUARD(ok, site, ctrl, tile)
 #endif
-#ifndef FLRL_RL_LAG_INLINE
-#define RL_LAG_CALL __noinline__
-#else
-#define RL_LAG_CALL __forceinline__
-#endif
 
-// Pointers into LDS and global memory that keep their address space across
-// the out-of-line calls below: passed as plain pointers, a callee sees generic
-// ones and every access becomes a flat instruction (LDS reads and global
-// stores alike); cast back to generic at the callee's top, the compiler infers
-// the space again and emits ds_ / global_ instructions.
+// Pointers into LDS and global memory typed with their address space at the
+// helpers' boundaries (once out-of-line calls: with plain pointers a callee saw
+// generic ones, every access became a flat instruction, and the build faulted
+// on the GPU with an aperture violation; inlined now, the types keep the
+// helpers' accesses ds_ / global_ whatever the caller's pointer provenance).
 typedef __attribute__((address_space(3))) uint8_t lds_u8;
 typedef __attribute__((address_space(3))) uint64_t lds_u64;
 typedef __attribute__((address_space(1))) uint8_t glb_u8;
@@ -1163,32 +1186,34 @@ struct RlChunkInfo {
 };
 constexpr uint32_t kRlOverflow = 0x100u;
 
-// Emission of a whole tile whose runs are all staged, by the look-back wave
-// alone, with the tile's state st (heads before it, chunk state at its start):
-// chunk by chunk its split heads (255, v0), the run of its first natural head
-// (count from the incoming state) and the staged runs, as 16-byte stores.
-template <class Wv, int W>
-__device__ void rl_emit_staged_tile(const uint8_t *__restrict__ in, uint64_t n, uint8_t *stg, const RlChunkInfo *info, const uint64_t *maps,
-                                    uint32_t tile, uint64_t st, uint8_t *__restrict__ counts,
-                                    uint8_t *__restrict__ values, uint64_t *__restrict__ runs_out, Ctrl *ctrl)
+// Emission of chunk v of a tile whose runs are all staged (sc: that chunk's
+// staging slice, counts then values), with the chunk's state st (heads before
+// it, chunk state at its start), by one wave: its split heads (255, v0), the
+// run of its first natural head (count from the incoming state) and the
+// staged runs, as 16-byte stores; the final run if the chunk ends the input.
+template <class Wv>
+__device__ __forceinline__ void rl_emit_staged_chunk(const uint8_t *__restrict__ in, uint64_t n, uint8_t *sc,
+                                                     const RlChunkInfo &info, uint32_t tile, int v, uint64_t st,
+                                                     uint8_t *__restrict__ counts, uint8_t *__restrict__ values,
+                                                     uint64_t *__restrict__ runs_out, Ctrl *ctrl)
 {
-    const int lane = threadIdx.x & (kWave - 1);
-#pragma unroll 1
-    for (int v = 0; v < W; ++v) {
+    int lane = threadIdx.x & (kWave - 1);
+    asm volatile("" : "+v"(lane));  // lane-derived addresses stay inside the caller's loop iteration
+    const uint64_t off = (uint64_t)tile * Wv::TBT + (uint64_t)v * Wv::CB;
+    if (off >= n)
+        return;
+    do {
         RL_LAG_GUARD(sm_h(st) <= n && (st & kSmKind) == kSmConst, 0, ctrl, tile)
-        const uint64_t off = (uint64_t)tile * Wv::TBT + (uint64_t)v * Wv::CB;
-        if (off >= n)
-            break;
         const uint32_t len = n - off < (uint64_t)Wv::CB ? (uint32_t)(n - off) : (uint32_t)Wv::CB;
-        const uint32_t first = uniform32(info[v].first), K = uniform32(info[v].K);
-        const uint32_t rel_in = uniform32(info[v].rel_in), v0 = uniform32(info[v].v0) & 0xFFu;
-        const uint64_t h_in = sm_h(st);
-        const uint32_t c_in = sm_c(st);
+        const uint32_t first = uniform32(info.first), K = uniform32(info.K);
+        const uint32_t rel_in = uniform32(info.rel_in), v0 = uniform32(info.v0) & 0xFFu;
+        const uint64_t h_in = uniform64(sm_h(st));
+        const uint32_t c_in = uniform32(sm_c(st));
         const uint32_t pre = first != Wv::kNone ? first : len;
         const uint32_t S = splits(c_in, pre);
+        RL_LAG_GUARD(K <= Wv::SW && S <= 130 && h_in + S + K <= n, 1, ctrl, tile)
         // split heads h_in + j (j < S) end 255-byte pieces of v0; record g is
         // output byte g - 1 (record 0, the input's first head, ends no run)
-        RL_LAG_GUARD(K <= Wv::SW && S <= 130 && h_in + S + K <= n, 1, ctrl, tile)
         {
             const uint64_t g = h_in == 0 ? 1 : h_in, e = h_in + S;
             if (e > g) {
@@ -1198,7 +1223,6 @@ __device__ void rl_emit_staged_tile(const uint8_t *__restrict__ in, uint64_t n, 
         }
         const uint64_t g0 = h_in + S;  // record of the first natural head
         if (K) {
-            uint8_t *const sc = stg + v * 2 * Wv::SW;
             uint8_t *const sv = sc + Wv::SW;
             if (lane == 0) {
                 const uint32_t c = add_c(c_in, first);
@@ -1216,29 +1240,27 @@ __device__ void rl_emit_staged_tile(const uint8_t *__restrict__ in, uint64_t n, 
             values[R - 1] = in[n - 1];
             *runs_out = R;
         }
-        st = sm_compose(st, maps[v]);
-    }
+    } while (false);
 }
 
 // The look-back wave's part of a tile (persistent form): publish the tile's
-// map, resolve its state, then emit its staged runs -- or, when a chunk's
-// staging overflowed, hand the chunks' states to the data waves (s_st). Kept
-// out of line, as is the data waves' emission of overflowed tiles: inlined,
-// their registers added to the scan loop's and the kernel spilled.
+// map, resolve its state, then either emit its staged runs itself
+// (FLRL_RL_LAG_EMIT 0) or hand every chunk's state to the data waves (s_st:
+// always for a tile whose staging overflowed, as its data waves re-read it).
+// Inlined into the look-back wave's own loop: the kernel must use no scratch
+// at all (a call's saved registers live there, and a kernel with scratch got
+// fewer workgroups per CU than its persistent grid, see below).
 template <class Wv, int W>
-__device__ RL_LAG_CALL void rl_lag_resolve(const glb_u8 *in_g, uint64_t n, lds_u8 *stg_l, lds_u8 *info_l,
-                                           lds_u8 *maps_l, lds_u8 *st_l, bool ovf, uint32_t tile,
-                                           glb_u8 *counts_g, glb_u8 *values_g, glb_u64 *runs_g, glb_u8 *ctrl_g,
-                                           glb_u64 *status_g, uint64_t help_ticks)
+__device__ __forceinline__ void rl_lag_resolve(const glb_u8 *in_g, uint64_t n, lds_u8 *stg_l, lds_u8 *info_l,
+                                               lds_u8 *maps_l, lds_u8 *st_l, bool ovf, uint32_t tile,
+                                               glb_u8 *counts_g, glb_u8 *values_g, glb_u64 *runs_g, glb_u8 *ctrl_g,
+                                               glb_u64 *status_g, uint64_t help_ticks)
 {
     const uint8_t *const in = (const uint8_t *)in_g;
     uint8_t *const stg = (uint8_t *)stg_l;
     const RlChunkInfo *const info = (const RlChunkInfo *)(uint8_t *)info_l;
     const uint64_t *const maps = (const uint64_t *)(uint8_t *)maps_l;
     uint64_t *const s_st = (uint64_t *)(uint8_t *)st_l;
-    uint8_t *const counts = (uint8_t *)counts_g;
-    uint8_t *const values = (uint8_t *)values_g;
-    uint64_t *const runs_out = (uint64_t *)runs_g;
     Ctrl *const ctrl = (Ctrl *)(uint8_t *)ctrl_g;
     uint64_t *const status = (uint64_t *)status_g;
     uint64_t tmap = maps[0];
@@ -1250,7 +1272,7 @@ __device__ RL_LAG_CALL void rl_lag_resolve(const glb_u8 *in_g, uint64_t n, lds_u
     auto help = [&](uint32_t t) -> uint64_t { return rl_tile_map_slow<Wv::TBT>(in, n, t); };
     uint64_t st = lookback_seg<kRlLookG, kRlLookL, kRlStatusStride>(status, tile, tmap, ctrl, help_ticks, help);
     FLRL_RL_TRACE(tile, 3);
-    if (ovf) {
+    if (FLRL_RL_LAG_EMIT || ovf) {
         if ((threadIdx.x & (kWave - 1)) == 0) {
 #pragma unroll
             for (int v = 0; v < W; ++v) {
@@ -1259,67 +1281,57 @@ __device__ RL_LAG_CALL void rl_lag_resolve(const glb_u8 *in_g, uint64_t n, lds_u
             }
         }
     } else {
-        rl_emit_staged_tile<Wv, W>(in, n, stg, info, maps, tile, st, counts, values, runs_out, ctrl);
+        uint8_t *const counts = (uint8_t *)counts_g;
+        uint8_t *const values = (uint8_t *)values_g;
+        uint64_t *const runs_out = (uint64_t *)runs_g;
+#pragma unroll 1
+        for (int v = 0; v < W; ++v) {
+            rl_emit_staged_chunk<Wv>(in, n, stg + v * 2 * Wv::SW, info[v], tile, v, st, counts, values, runs_out,
+                                     ctrl);
+            st = sm_compose(st, maps[v]);
+        }
         FLRL_RL_TRACE(tile, 4);
     }
 }
 
-// A data wave's emission of its chunk of an overflowed tile, the chunk's facts
-// read back from LDS (nothing of the scan stays live across the loop).
-template <class Wv>
-__device__ RL_LAG_CALL void rl_emit_overflowed(const glb_u8 *in_g, uint64_t n, lds_u8 *img_l, int w, lds_u8 *stg_l,
-                                               lds_u8 *info_l, uint32_t tile, uint64_t st, glb_u8 *counts_g,
-                                               glb_u8 *values_g, glb_u64 *runs_g)
-{
-    const uint8_t *const in = (const uint8_t *)in_g;
-    uint8_t *const stg = (uint8_t *)stg_l;
-    const RlChunkInfo &I = *(const RlChunkInfo *)(uint8_t *)info_l;
-    uint8_t *const counts = (uint8_t *)counts_g;
-    uint8_t *const values = (uint8_t *)values_g;
-    uint64_t *const runs_out = (uint64_t *)runs_g;
-    Wv V(in, n, (uint8_t *)img_l, w);
-    typename Wv::Chunk C;
-    C.off = uniform64((uint64_t)tile * Wv::TBT + (uint64_t)V.wi * Wv::CB);
-    C.len = C.off >= V.n ? 0u : (V.n - C.off < (uint64_t)Wv::CB ? (uint32_t)(V.n - C.off) : (uint32_t)Wv::CB);
-    C.ns = (int)((C.len + Wv::WB - 1) / Wv::WB);
-    C.nst = (int)uniform32(I.nst);
-    C.first = uniform32(I.first);
-    C.K = uniform32(I.K);
-    C.Kst = uniform32(I.Kst);
-    C.rel_in = uniform32(I.rel_in);
-    C.rel_st = uniform32(I.rel_st);
-    C.v0 = uniform32(I.v0) & 0xFFu;
-    V.stage_at(stg);
-    V.emit(C, sm_h(st), sm_c(st), counts, values, runs_out);
-}
-
 // Persistent form: one workgroup per slot (FLRL_RL_LAG_PER_CU per CU), W data
-// waves + one look-back wave. The data waves only scan: tile i's chunks into
-// staging buffer i mod 2, its maps and chunk facts to LDS, ONE barrier, then
-// straight on to tile i+1. Meanwhile the look-back wave publishes tile i,
-// resolves its state and emits its staged runs itself (16-byte stores), and
-// takes the ticket of tile i+2 -- so the data waves never wait for a
-// look-back unless it outlasts a whole tile scan. A tile whose staging
+// waves + one look-back wave. The data waves scan tile i's chunks into staging
+// buffer i mod 2 and leave its maps and chunk facts in LDS; ONE barrier per
+// tile; then they go straight on to tile i+1 while the look-back wave
+// publishes tile i and resolves its state (and takes the ticket of tile i+2).
+// Tile i's staged runs leave either by the look-back wave (FLRL_RL_LAG_EMIT 0)
+// or by the data waves at the top of their next tile, each its own chunk
+// (FLRL_RL_LAG_EMIT 1: the look-back wave then issues no stores, so its
+// atomics and polls never wait for stores to drain). A tile whose staging
 // overflowed (dense runs: sub-chunks to re-read with the true states) is
 // emitted by its data waves as in rl_encode_wave_kernel, after a second
 // barrier at which the look-back wave hands over the states. The first tile of
-// a workgroup is its index, the rest by ticket (the ticket of the tile after
-// next is taken while this one is scanned, so its round trip is hidden).
-template <int T, int LB, int SUB, int STG>
-__global__ __launch_bounds__(T + kWave, FLRL_RL_LAG_WPS) void rl_encode_lag_kernel(
+// a workgroup is its index, the rest by ticket.
+template <int W, int LB, int SUB, int STG>
+__global__ __launch_bounds__(kWave * (W + 1), FLRL_RL_LAG_WPS) void rl_encode_lag_kernel(
     const uint8_t *__restrict__ in, uint64_t n, uint32_t ntiles, uint8_t *__restrict__ counts,
     uint8_t *__restrict__ values, uint64_t *__restrict__ runs_out, Ctrl *ctrl, uint64_t *status,
     uint64_t help_ticks)
 {
-    constexpr int W = T / kWave;
-    using Wv = RlWave<LB, SUB, W, STG>;
+    using Wv = RlWave<LB, SUB, W, STG, FLRL_RL_LAG_PF>;
     constexpr int kStg = STG + 32;  // + the flush's read slack
+    constexpr bool kDataEmit = FLRL_RL_LAG_EMIT != 0;
     __shared__ __attribute__((aligned(16))) uint8_t s_img[W * Wv::WB];
     __shared__ __attribute__((aligned(16))) uint8_t s_stg[2][kStg];
     __shared__ uint64_t s_map[2][W];
     __shared__ RlChunkInfo s_info[2][W];
-    __shared__ uint64_t s_st[W];
+    __shared__ uint64_t s_st[2][W];
     __shared__ uint32_t s_tile[2];
+    __shared__ uint32_t s_prev[2][W];
+    // the arguments only the emission paths need, parked in LDS: re-read after
+    // each barrier, they hold no scalar registers across the scan loop
+    struct Args {
+        uint8_t *counts, *values;
+        uint64_t *runs_out, *status;
+        Ctrl *ctrl;
+        uint64_t help_ticks;
+    };
+    __shared__ Args s_args;
 
     const int tid = threadIdx.x;
     const int w = __builtin_amdgcn_readfirstlane(tid / kWave);
@@ -1328,21 +1340,24 @@ __global__ __launch_bounds__(T + kWave, FLRL_RL_LAG_WPS) void rl_encode_lag_kern
     uint32_t tile = blockIdx.x;
     if (tile >= ntiles)
         return;
+    if (tid == 0)
+        s_args = Args{counts, values, runs_out, status, ctrl, help_ticks};
     // a tile ticket: tiles from gridDim.x on. A launch draws exactly ntiles
     // tickets (each workgroup until its first past the end), so a raw ticket
     // >= ntiles means the scratch's counter was not reset for this launch.
-    auto ticket = [&]() -> uint32_t {
-        const uint32_t raw = atomicAdd(&ctrl->ticket, 1u);
+    auto ticket = [&](Ctrl *c) -> uint32_t {
+        const uint32_t raw = atomicAdd(&c->ticket, 1u);
         if (raw >= ntiles) {
-            raise_error(ctrl, FLRL_E_ARG);
+            raise_error(c, FLRL_E_ARG);
             return ntiles;
         }
         const uint64_t t = (uint64_t)raw + gridDim.x;
         return t < ntiles ? (uint32_t)t : ntiles;
     };
     if (lw && V.lane == 0)
-        s_tile[1] = ticket();
+        s_tile[1] = ticket(ctrl);
     auto scan = [&](uint32_t t, int b) {
+        V.relane();
         V.stage_at(s_stg[b]);
         const uint64_t off = (uint64_t)t * Wv::TBT + (uint64_t)w * Wv::CB;
         typename Wv::Chunk C;
@@ -1353,38 +1368,103 @@ __global__ __launch_bounds__(T + kWave, FLRL_RL_LAG_WPS) void rl_encode_lag_kern
                                        (uint32_t)C.nst, C.Kst, C.rel_st, 0u};
         }
     };
-    FLRL_RL_TRACE(tile, 0);
-    if (!lw)
-        scan(tile, 0);
-    int b = 0;
-    for (;;) {
-        __syncthreads();  // tile scanned into staging b; s_tile[b ^ 1] = the next tile
-        FLRL_RL_TRACE(tile, 1);
-        const uint32_t nxt = s_tile[b ^ 1];
+    auto tile_overflowed = [&](int b) {
         bool ovf = false;
 #pragma unroll
         for (int v = 0; v < W; ++v)
             ovf |= (s_info[b][v].v0 & kRlOverflow) != 0;
-        if (lw) {
-            // s_tile[b] was last read before the barrier above
-            if (nxt < ntiles && V.lane == 0)
-                s_tile[b] = ticket();
-            rl_lag_resolve<Wv, W>((const glb_u8 *)in, n, as_lds(s_stg[b]), as_lds(s_info[b]), as_lds(s_map[b]),
-                                  as_lds(s_st), ovf, tile, as_glb(counts), as_glb(values), as_glb(runs_out),
-                                  (glb_u8 *)ctrl, as_glb(status), help_ticks);
-        }
-        if (ovf) {
-            __syncthreads();  // the chunks' states in s_st
-            if (!lw)
-                rl_emit_overflowed<Wv>((const glb_u8 *)in, n, as_lds(s_img), w, as_lds(s_stg[b]), as_lds(&s_info[b][w]),
-                                       tile, s_st[w], as_glb(counts), as_glb(values), as_glb(runs_out));
-        }
-        if (nxt >= ntiles)
-            break;
-        if (!lw)
+        return ovf;
+    };
+    FLRL_RL_TRACE(tile, 0);
+    // The two roles run separate loops with the same barrier sequence per tile
+    // (A: the tile is scanned; B, only when a chunk's staging overflowed: the
+    // states are in s_st; with FLRL_RL_LAG_EMIT 1 and a last tile that did not
+    // overflow, one more at the end: its states), so each loop's registers are
+    // allocated on their own: one loop holding both roles' live values spilled
+    // to scratch, and a kernel with scratch is dispatched with fewer
+    // workgroups per CU than the persistent grid assumes.
+    if (!lw) {
+        // the data waves' emission of their own chunk of a staged tile
+        auto emit_staged = [&](uint32_t t, int b) {
+            const Args a = s_args;
+            rl_emit_staged_chunk<Wv>(in, n, s_stg[b] + w * 2 * Wv::SW, s_info[b][w], t, w, s_st[b][w], a.counts,
+                                     a.values, a.runs_out, a.ctrl);
+        };
+        // s_prev[x][w]: the tile in staging x whose staged runs this wave still
+        // has to emit (kNone: none), kept in LDS rather than in registers
+        if (V.lane == 0)
+            s_prev[1][w] = Wv::kNone;
+        scan(tile, 0);
+        int b = 0;
+        for (;;) {
+            __syncthreads();  // A: tile scanned into staging b; s_tile[b ^ 1] = the next tile
+            const uint32_t nxt = s_tile[b ^ 1];
+            const bool ovf = tile_overflowed(b);
+            if (kDataEmit) {  // the previous tile (staging b ^ 1; its states came before A), if staged
+                const uint32_t prev = uniform32(s_prev[b ^ 1][w]);
+                if (prev != Wv::kNone)
+                    emit_staged(prev, b ^ 1);
+                if (V.lane == 0)
+                    s_prev[b][w] = ovf ? Wv::kNone : tile;
+            }
+            if (ovf) {
+                __syncthreads();  // B: the chunks' states in s_st[b]
+                // the chunk's facts back from LDS (nothing of the scan is live
+                // across the loop), then the emission of rl_encode_wave_kernel
+                const Args a = s_args;
+                const RlChunkInfo &I = s_info[b][w];
+                typename Wv::Chunk C;
+                C.off = (uint64_t)tile * Wv::TBT + (uint64_t)w * Wv::CB;
+                C.len = C.off >= n ? 0u : (n - C.off < (uint64_t)Wv::CB ? (uint32_t)(n - C.off) : (uint32_t)Wv::CB);
+                C.ns = (int)((C.len + Wv::WB - 1) / Wv::WB);
+                C.nst = (int)uniform32(I.nst);
+                C.first = uniform32(I.first);
+                C.K = uniform32(I.K);
+                C.Kst = uniform32(I.Kst);
+                C.rel_in = uniform32(I.rel_in);
+                C.rel_st = uniform32(I.rel_st);
+                C.v0 = uniform32(I.v0) & 0xFFu;
+                const uint64_t st = s_st[b][w];
+                V.relane();
+                V.stage_at(s_stg[b]);
+                V.emit(C, sm_h(st), sm_c(st), a.counts, a.values, a.runs_out);
+            }
+            if (nxt >= ntiles) {
+                if (kDataEmit && !ovf) {
+                    __syncthreads();  // C: the last tile's states in s_st[b]
+                    emit_staged(tile, b);
+                }
+                break;
+            }
+            FLRL_RL_TRACE(nxt, 0);
             scan(nxt, b ^ 1);
-        tile = nxt;
-        b ^= 1;
+            tile = nxt;
+            b ^= 1;
+        }
+    } else {
+        int b = 0;
+        for (;;) {
+            __syncthreads();  // A
+            FLRL_RL_TRACE(tile, 1);
+            const uint32_t nxt = s_tile[b ^ 1];
+            const bool ovf = tile_overflowed(b);
+            // s_tile[b] was last read before barrier A
+            const Args a = s_args;
+            if (nxt < ntiles && V.lane == 0)
+                s_tile[b] = ticket(a.ctrl);
+            rl_lag_resolve<Wv, W>((const glb_u8 *)in, n, as_lds(s_stg[b]), as_lds(s_info[b]), as_lds(s_map[b]),
+                                  as_lds(s_st[b]), ovf, tile, as_glb(a.counts), as_glb(a.values), as_glb(a.runs_out),
+                                  (glb_u8 *)a.ctrl, as_glb(a.status), a.help_ticks);
+            if (ovf)
+                __syncthreads();  // B
+            if (nxt >= ntiles) {
+                if (kDataEmit && !ovf)
+                    __syncthreads();  // C
+                break;
+            }
+            tile = nxt;
+            b ^= 1;
+        }
     }
 }
 
@@ -2033,7 +2113,7 @@ struct RlEncLayout {
     size_t tiles, zero, bytes;
     explicit RlEncLayout(size_t n)
     {
-        tiles = div_up(n, (size_t)kRlTileBytes);
+        tiles = div_up(n, (size_t)kRlEncTileBytes);
         zero = kRlStatusOff + round_up(tiles * 8 * kRlStatusStride, 16);  // ticket, error, status
         bytes = zero;
     }
@@ -2097,8 +2177,8 @@ extern "C" int flrl_rl_encode_device(const uint8_t *d_in, size_t n, uint8_t *d_c
     kernel_timing_begin(s);
     if (FLRL_RL_LAG) {
         const size_t slots = (size_t)FLRL_RL_LAG_PER_CU * (size_t)cu_count();
-        hipLaunchKernelGGL((rl_encode_lag_kernel<kRlThreads, kRlLaneBytes, kRlSub, FLRL_RL_LAG_STAGE>),
-                           dim3((uint32_t)(L.tiles < slots ? L.tiles : slots)), dim3(kRlThreads + kWave), 0, s, d_in,
+        hipLaunchKernelGGL((rl_encode_lag_kernel<kRlLagWaves, kRlLaneBytes, kRlSub, FLRL_RL_LAG_STAGE>),
+                           dim3((uint32_t)(L.tiles < slots ? L.tiles : slots)), dim3(kRlLagThreads), 0, s, d_in,
                            (uint64_t)n, (uint32_t)L.tiles, d_counts, d_values, d_runs, ctrl, status,
                            lookback_help_ticks(kRlHelpTicks));
     } else {

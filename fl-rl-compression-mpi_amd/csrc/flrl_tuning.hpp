@@ -17,7 +17,7 @@
      defined(FLRL_RL_STAGE) || defined(FLRL_RL_WPS) || defined(FLRL_RD_NARROW_MEAN) || defined(FLRL_RL_RO_MAXB) ||          \
      defined(FLRL_RD_UNROLL) || defined(FLRL_HOST_WORKERS) || defined(FLRL_HOST_CHUNK) ||                \
      defined(FLRL_HOST_DIRECT) || defined(FLRL_HOST_PROFILE) || defined(FLRL_HOST_THP) || defined(FLRL_RL_WD64_MEAN) || defined(FLRL_RL_DENSE_MEAN) ||\
-     defined(FLRL_RL_LAG) || defined(FLRL_RL_LAG_WPS) || defined(FLRL_RL_LAG_PER_CU) || defined(FLRL_RL_LAG_STAGE) || defined(FLRL_RL_LAG_GUARD) || defined(FLRL_RL_LAG_INLINE))
+     defined(FLRL_RL_LAG) || defined(FLRL_RL_LAG_WPS) || defined(FLRL_RL_LAG_PER_CU) || defined(FLRL_RL_LAG_STAGE) || defined(FLRL_RL_LAG_GUARD) || defined(FLRL_RL_LAG_WAVES) || defined(FLRL_RL_LAG_EMIT) || defined(FLRL_RL_LAG_PF))
 #error "FLRL_* kernel overrides are for timing harnesses only (define FLRL_TUNING_BUILD)"
 #endif
 
@@ -90,17 +90,31 @@
 #ifndef FLRL_RL_LAG
 #define FLRL_RL_LAG 0
 #endif
-// persistent form: workgroups (4 data waves + the look-back wave) per CU, the
-// waves per SIMD they are compiled for, and each of the two staging buffers
-// (bytes per workgroup; 4 per CU leave 2 x 12032 beside the 16 KiB images)
+// persistent form: data waves per workgroup (+ the look-back wave: 4 waves,
+// one per SIMD -- a 5-wave workgroup of 4 data waves placed unevenly, and only
+// two per CU were ever resident), workgroups per CU, the waves per SIMD they
+// are compiled for, and each of the two staging buffers (bytes per workgroup;
+// five per CU leave 2 x 9600 beside the 12 KiB images)
+#ifndef FLRL_RL_LAG_WAVES
+#define FLRL_RL_LAG_WAVES 3
+#endif
 #ifndef FLRL_RL_LAG_PER_CU
-#define FLRL_RL_LAG_PER_CU 4
+#define FLRL_RL_LAG_PER_CU 5
 #endif
 #ifndef FLRL_RL_LAG_WPS
 #define FLRL_RL_LAG_WPS 5
 #endif
 #ifndef FLRL_RL_LAG_STAGE
-#define FLRL_RL_LAG_STAGE 12032
+#define FLRL_RL_LAG_STAGE 9600
+#endif
+// persistent form: staged runs emitted by the data waves at the top of their
+// next tile (1) or by the look-back wave (0)
+#ifndef FLRL_RL_LAG_EMIT
+#define FLRL_RL_LAG_EMIT 1
+#endif
+// persistent form: sub-chunks in flight per data wave
+#ifndef FLRL_RL_LAG_PF
+#define FLRL_RL_LAG_PF FLRL_RL_PF
 #endif
 
 // ---- RL decode shape ---------------------------------------------------------

@@ -12,7 +12,7 @@ TAG=${1:-r01}
 shift
 BENCH_ARGS=("$@")
 # the 16 GiB north-star launches would mix into the 1 GiB kernel averages: profile them separately
-[ ${#BENCH_ARGS[@]} -eq 0 ] && BENCH_ARGS=(--no-north-star --no-rl-dense)
+[ ${#BENCH_ARGS[@]} -eq 0 ] && BENCH_ARGS=(--no-north-star --no-rl-dense --no-configs3)
 OUT=gpurun_out/prof/$TAG
 mkdir -p "$OUT"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run \

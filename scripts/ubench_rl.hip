@@ -50,7 +50,7 @@ __device__ __forceinline__ uint64_t rl_rtime()
 }
 #define FLRL_RL_TRACE(tile, k)                                                   \
     do {                                                                         \
-        if (threadIdx.x == 0)                                                    \
+        if ((threadIdx.x & 63) == 0)                                             \
             g_trace[(uint64_t)(tile) * 8 + (k)] = rl_rtime(); \
     } while (0)
 #define FLRL_RL_LB_STAT(tile, spins, rounds)                                      \
@@ -108,7 +108,7 @@ int main(int argc, char **argv)
         free(h);
     }
 #ifdef TRACE
-    const size_t ntiles = (n + 131071) / 131072;
+    const size_t ntiles = (n + flrl::kRlEncTileBytes - 1) / flrl::kRlEncTileBytes;  // tiles of the shipped form
     uint64_t *d_tr;
     CK(hipMalloc(&d_tr, ntiles * 64));
     CK(hipMemset(d_tr, 0, ntiles * 64));
