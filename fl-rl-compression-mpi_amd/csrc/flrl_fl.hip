@@ -300,9 +300,15 @@ __global__ __launch_bounds__(T + kWave, 1) void fl_encode_kernel(
             if (tile + 1 < ntiles) {
                 // static trip count: LDS reads hoisted, stores predicated; in two
                 // halves, as the registers also hold the prefetched tile
-                constexpr int SPLIT = 2;
+                constexpr int SPLIT = FLRL_FL_STORE_SPLIT;
 #pragma unroll
                 for (int h = 0; h < SPLIT; ++h) {
+#if FLRL_FL_STORE_SKIP
+                    // a part of the staging tile past the tile's packed bytes
+                    // (agg is uniform: widths below 8) is neither read nor stored
+                    if (h > 0 && agg <= (uint32_t)(h * (ITEMS / SPLIT) * T))
+                        break;
+#endif
                     u32x4 o[ITEMS / SPLIT];
 #pragma unroll
                     for (int k = 0; k < ITEMS / SPLIT; ++k)
