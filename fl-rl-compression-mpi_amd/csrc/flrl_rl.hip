@@ -49,7 +49,7 @@ namespace flrl {
 
 constexpr int kRlThreads = FLRL_RL_THREADS;         // encode workgroup: 4 waves (LB 64: 94 VGPRs, < 32 KiB LDS, 5 per CU)
 constexpr int kRlLaneBytes = 64;                    // contiguous bytes per lane (a u64 head mask)
-constexpr int kRlSub = 32768 / (64 * kRlLaneBytes); // sub-chunks per wave chunk (one look-back per tile)
+constexpr int kRlSub = FLRL_RL_SUB;                 // sub-chunks of 4 KiB per wave chunk (one look-back per tile)
 constexpr int kRlTileBytes = kRlLaneBytes * kRlThreads * kRlSub;  // 128 KiB: 4 waves x 32 KiB
 // persistent form (rl_encode_lag_kernel): FLRL_RL_LAG_WAVES data waves of 32 KiB
 // chunks + the look-back wave per workgroup

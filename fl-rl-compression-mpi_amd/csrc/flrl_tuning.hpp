@@ -18,7 +18,7 @@
      defined(FLRL_RD_UNROLL) || defined(FLRL_HOST_WORKERS) || defined(FLRL_HOST_CHUNK) ||                \
      defined(FLRL_HOST_DIRECT) || defined(FLRL_HOST_PROFILE) || defined(FLRL_HOST_THP) || defined(FLRL_RL_WD64_MEAN) || defined(FLRL_RL_DENSE_MEAN) ||\
      defined(FLRL_RL_LAG) || defined(FLRL_RL_LAG_WPS) || defined(FLRL_RL_LAG_PER_CU) || defined(FLRL_RL_LAG_STAGE) || defined(FLRL_RL_LAG_GUARD) || defined(FLRL_RL_LAG_WAVES) || defined(FLRL_RL_LAG_EMIT) || defined(FLRL_RL_LAG_PF) ||\
-     defined(FLRL_FL_STORE_SPLIT) || defined(FLRL_FL_STORE_SKIP))
+     defined(FLRL_FL_STORE_SPLIT) || defined(FLRL_FL_STORE_SKIP) || defined(FLRL_RL_SUB))
 #error "FLRL_* kernel overrides are for timing harnesses only (define FLRL_TUNING_BUILD)"
 #endif
 
@@ -42,6 +42,9 @@
 // ---- RL encode shape ---------------------------------------------------------
 #ifndef FLRL_RL_THREADS
 #define FLRL_RL_THREADS 256  // 4 waves (LB 64: 94 VGPRs, < 32 KiB LDS, 5 per CU)
+#endif
+#ifndef FLRL_RL_SUB
+#define FLRL_RL_SUB 8  // RL encode: 4 KiB sub-chunks per wave chunk (8: 32 KiB chunks, 128 KiB tiles)
 #endif
 #ifndef FLRL_FL_LOOKG
 #define FLRL_FL_LOOKG 1  // FL encode look-back granules per lane (window 64 G tiles)
