@@ -791,12 +791,25 @@ struct RlWave {
             const uint32_t hi = span - 16 * q < 16 ? span - 16 * q : 16u;
 #pragma unroll
             for (int arr = 0; arr < 2; ++arr) {
+#if FLRL_ABL_FLUSH == 1  // timing-only ablation: no LDS gather
+                const u32x4 v = u32x4{(uint32_t)o, 1u, 2u, 3u};
+#else
                 const u32x4 v = piece_gather(arr ? stv : stc, o);
+#endif
                 uint8_t *const d = (arr ? pv : pc) + 16 * q;
-                if (lo == 0 && hi == 16)
+#if FLRL_ABL_FLUSH == 2  // timing-only ablation: no stores
+                asm volatile("" ::"v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]));
+                continue;
+#endif
+                if (lo == 0 && hi == 16) {
+#if FLRL_RL_FLUSH_NT
+                    __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(d));
+#else
                     *reinterpret_cast<u32x4 *>(d) = v;
-                else
+#endif
+                } else {
                     store_chunk_part(d, v, lo, hi);
+                }
             }
         }
     }
@@ -933,6 +946,10 @@ struct RlWave {
                 // four parts of 16 rows (<= 1024 records each, within the staging),
                 // each staged by piece_part and stored with 16-byte stores
                 const uint32_t sl = (uint32_t)(g - hb);
+#if FLRL_RL_DENSE_PF_EARLY
+                if (s + 1 < ns)
+                    load_sub(off, s + 1, pf);  // in flight across the pieces' stores
+#endif
 #pragma unroll 1
                 for (int p = 0; p < kWave / 16; ++p) {
                     const uint32_t b0 = (uint32_t)__builtin_amdgcn_readlane((int)sl, 16 * p);
@@ -943,7 +960,7 @@ struct RlWave {
                     wave_lds_sync();
                 }
             }
-            if (hs > (uint32_t)SW && s + 1 < ns)
+            if (!FLRL_RL_DENSE_PF_EARLY && hs > (uint32_t)SW && s + 1 < ns)
                 load_sub(off, s + 1, pf);  // after the pieces: see above
             hb += hs;
             rel = pm_compose(rel, L.smap);
@@ -2094,7 +2111,11 @@ __global__ __launch_bounds__(kWdThreads) void rl_decode_wave_kernel(
                     const uint32_t lo = gq < b0 ? b0 - gq : 0u;
                     const uint32_t hi = gq + 16 > len ? len - gq : 16u;
                     if (lo == 0 && hi == 16)
+#if FLRL_RD_WAVE_NT
+                        __builtin_nontemporal_store(ov, reinterpret_cast<u32x4 *>(out + g0 + gq));
+#else
                         *reinterpret_cast<u32x4 *>(out + g0 + gq) = ov;  // plain stores, as the block decode
+#endif
                     else  // a chunk shared with a neighbouring tile: its bytes only
                         store_chunk_part(out + g0 + gq, ov, lo, hi);
                 }

@@ -182,7 +182,7 @@ int main(int argc, char **argv)
         CK(hipDeviceSynchronize());
         uint64_t *h = (uint64_t *)malloc(ntiles * 64);
         CK(hipMemcpy(h, d_tr, ntiles * 64, hipMemcpyDeviceToHost));
-        FILE *f = fopen("gpurun_out/rl_trace.bin", "wb");
+        FILE *f = fopen(getenv("TRACE_OUT") ? getenv("TRACE_OUT") : "gpurun_out/rl_trace.bin", "wb");
         if (f) {
             fwrite(h, 64, ntiles, f);
             fclose(f);
