@@ -31,3 +31,13 @@ print("tile starts per us (steady state):", round(len(t) / (start.max() - start.
 tail = end.max() - np.percentile(end, 99)
 print(f"last 1 % of stores issued over {tail:.1f} us; start-up: 99 % of first-round tiles started by "
       f"{np.percentile(start[:256], 99):.1f} us")
+# launch overhead against the steady state: tiles completed per us over the
+# middle 80 % of completions, the span that rate would need for all tiles,
+# and where the rest goes (ramp: first completion; tail: last 256 completions)
+done = np.sort(end)
+k0, k1 = int(0.1 * len(done)), int(0.9 * len(done))
+rate = (k1 - k0) / (done[k1] - done[k0])
+print(f"steady completions {rate:.2f} tiles/us -> ideal span {len(done) / rate:.1f} us vs {done[-1]:.1f} us; "
+      f"first completion {done[0]:.1f} us, 256th {done[min(255, len(done) - 1)]:.1f} us, "
+      f"last 256 completions over {done[-1] - done[max(0, len(done) - 256)]:.1f} us "
+      f"(steady: {256 / rate:.1f} us)")
