@@ -1868,8 +1868,12 @@ __global__ __launch_bounds__(T, 4) void rl_decode_kernel(  // 2nd: waves per SIM
                         const int32_t x = tb + (int32_t)x0;
                         if (x >= kRkWindow)
                             break;
+#if FLRL_ABL_RD & 2  // timing-only ablation: no start marks
+                        asm volatile("" ::"v"(x), "v"(x1));
+#else
                         if (x1 > x0 && x >= 0)
                             atomicOr(&s_bm[(uint32_t)x >> 5], 1u << (x & 31));
+#endif
                     }
                 }
                 __syncthreads();
@@ -1915,8 +1919,16 @@ __global__ __launch_bounds__(T, 4) void rl_decode_kernel(  // 2nd: waves per SIM
                     const uint32_t off = 16u * q;
                     if (off >= wl)
                         break;
+#if FLRL_ABL_RD & 1  // timing-only ablation: no chunk assembly
+                    const u32x4 o = u32x4{q, starts_before, 0u, 0u};
+#else
                     const u32x4 o = rd_chunk(s_bm, s_pre, reinterpret_cast<const uint32_t *>(s_val4), s_pfx, q,
                                              starts_before);
+#endif
+#if FLRL_ABL_RD & 4  // timing-only ablation: no output stores
+                    asm volatile("" ::"v"(o[0]), "v"(o[1]), "v"(o[2]), "v"(o[3]));
+                    continue;
+#endif
                     if (off >= b0 && off + 16 <= ce) {
                         *reinterpret_cast<u32x4 *>(outw + off) = o;  // plain: see the note above
                     } else {  // a chunk shared with a neighbouring tile: its bytes only

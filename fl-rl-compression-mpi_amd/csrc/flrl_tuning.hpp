@@ -18,7 +18,7 @@
      defined(FLRL_RD_UNROLL) || defined(FLRL_HOST_WORKERS) || defined(FLRL_HOST_CHUNK) ||                \
      defined(FLRL_HOST_DIRECT) || defined(FLRL_HOST_PROFILE) || defined(FLRL_HOST_THP) || defined(FLRL_RL_WD64_MEAN) || defined(FLRL_RL_DENSE_MEAN) ||\
      defined(FLRL_RL_LAG) || defined(FLRL_RL_LAG_WPS) || defined(FLRL_RL_LAG_PER_CU) || defined(FLRL_RL_LAG_STAGE) || defined(FLRL_RL_LAG_GUARD) || defined(FLRL_RL_LAG_WAVES) || defined(FLRL_RL_LAG_EMIT) || defined(FLRL_RL_LAG_PF) ||\
-     defined(FLRL_FL_STORE_SPLIT) || defined(FLRL_FL_STORE_SKIP) || defined(FLRL_RL_SUB) || defined(FLRL_RL_FLUSH_NT) || defined(FLRL_RD_WAVE_NT) || defined(FLRL_ABL_FLUSH) || defined(FLRL_RL_DENSE_PF_EARLY))
+     defined(FLRL_FL_STORE_SPLIT) || defined(FLRL_FL_STORE_SKIP) || defined(FLRL_RL_SUB) || defined(FLRL_RL_FLUSH_NT) || defined(FLRL_RD_WAVE_NT) || defined(FLRL_ABL_FLUSH) || defined(FLRL_RL_DENSE_PF_EARLY) || defined(FLRL_ABL_RD))
 #error "FLRL_* kernel overrides are for timing harnesses only (define FLRL_TUNING_BUILD)"
 #endif
 
@@ -57,6 +57,9 @@
 #endif
 #ifndef FLRL_RL_DENSE_PF_EARLY
 #define FLRL_RL_DENSE_PF_EARLY 0  // RL encode re-read: next sub-chunk's load issued before the dense pieces
+#endif
+#ifndef FLRL_ABL_RD
+#define FLRL_ABL_RD 0  // timing-only ablations of the RL block decode (1: no assembly, 2: no marks, 4: no stores)
 #endif
 #ifndef FLRL_FL_LOOKG
 #define FLRL_FL_LOOKG 1  // FL encode look-back granules per lane (window 64 G tiles)
