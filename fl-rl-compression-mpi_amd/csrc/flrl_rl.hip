@@ -1929,6 +1929,10 @@ __global__ __launch_bounds__(T, 4) void rl_decode_kernel(  // 2nd: waves per SIM
                     asm volatile("" ::"v"(o[0]), "v"(o[1]), "v"(o[2]), "v"(o[3]));
                     continue;
 #endif
+#if FLRL_ABL_RD & 8  // timing-only ablation: every chunk stored whole (no edge path)
+                    *reinterpret_cast<u32x4 *>(outw + off) = o;
+                    continue;
+#endif
                     if (off >= b0 && off + 16 <= ce) {
                         *reinterpret_cast<u32x4 *>(outw + off) = o;  // plain: see the note above
                     } else {  // a chunk shared with a neighbouring tile: its bytes only

@@ -59,7 +59,7 @@
 #define FLRL_RL_DENSE_PF_EARLY 0  // RL encode re-read: next sub-chunk's load issued before the dense pieces
 #endif
 #ifndef FLRL_ABL_RD
-#define FLRL_ABL_RD 0  // timing-only ablations of the RL block decode (1: no assembly, 2: no marks, 4: no stores)
+#define FLRL_ABL_RD 0  // timing-only ablations of the RL block decode (1: no assembly, 2: no marks, 4: no stores, 8: whole-chunk stores only)
 #endif
 #ifndef FLRL_FL_LOOKG
 #define FLRL_FL_LOOKG 1  // FL encode look-back granules per lane (window 64 G tiles)
