@@ -6,9 +6,9 @@
 //          thread t at chunk k*512 + t of the window
 //   tiles+work: the same with a VALU-only phase of `spin` iterations before
 //          each window's stores (the decode's marks and scan), barrier-separated
-//   work:  the phases alone, no stores (spin < 0: -spin LDS round trips per phase instead of VALU)
+//   work:  the phases alone, no stores (spin < 0: -spin LDS write+read round trips per phase instead of VALU; spin <= -1000: -(spin+1000) LDS reads only)
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 scripts/ubench_write.hip -o scripts/ubench_write.bin
-//   scripts/ubench_write.bin [spin=2000] [reps=20]
+//   scripts/ubench_write.bin [spin=2000] [reps=20] [gather=0: 1 = store data read from LDS, 2 = all gathers then all stores] [gridstride=0]
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -41,8 +41,13 @@ __device__ __forceinline__ uint32_t spin_work(uint32_t x, int spin)
             x = x * 1664525u + 1013904223u;
         return x;
     }
-    // spin < 0: -spin dependent LDS round trips (write, read back a neighbour's word)
     __shared__ uint32_t s_buf[T * 4];
+    if (spin <= -1000) {  // -(spin + 1000) dependent LDS reads, no LDS writes
+        for (int i = 0; i < -(spin + 1000); ++i)
+            x += s_buf[(threadIdx.x * 4 + i + (x & 63)) & (T * 4 - 1)] * 3u;
+        return x;
+    }
+    // spin < 0: -spin dependent LDS round trips (write, read back a neighbour's word)
     for (int i = 0; i < -spin; ++i) {
         s_buf[(threadIdx.x * 4 + i) & (T * 4 - 1)] = x;
         x += s_buf[(threadIdx.x * 4 + i + 64) & (T * 4 - 1)] * 3u;
@@ -50,26 +55,61 @@ __device__ __forceinline__ uint32_t spin_work(uint32_t x, int spin)
     return x;
 }
 
+__shared__ uint32_t s_gat[T * 8];
+
 template <bool STORE>
-__global__ __launch_bounds__(T, 4) void tiles_kernel(uint8_t *out, uint32_t ntiles, uint32_t *ticket, int spin)
+__global__ __launch_bounds__(T, 4) void tiles_kernel(uint8_t *out, uint32_t ntiles, uint32_t *ticket, int spin,
+                                                      int gather, int gridstride)
 {
     __shared__ uint32_t s_tile;
+    uint32_t gs_tile = blockIdx.x;
+    for (int i = threadIdx.x; i < T * 8; i += T)
+        s_gat[i] = i * 2654435761u;
     uint32_t x = threadIdx.x;
     for (;;) {
-        if (threadIdx.x == 0)
-            s_tile = atomicAdd(ticket, 1u);
-        __syncthreads();
-        const uint32_t tile = s_tile;
-        __syncthreads();
+        uint32_t tile;
+        if (gridstride) {  // no ticket: tiles blockIdx, blockIdx + grid, ...
+            tile = gs_tile;
+            gs_tile += gridDim.x;
+        } else {
+            if (threadIdx.x == 0)
+                s_tile = atomicAdd(ticket, 1u);
+            __syncthreads();
+            tile = s_tile;
+            __syncthreads();
+        }
         if (tile >= ntiles)
             break;
         for (uint64_t w = 0; w < kTile / kWin; ++w) {
             x = spin_work(x, spin);
             __syncthreads();
             u32x4 *o = reinterpret_cast<u32x4 *>(out + (uint64_t)tile * kTile + w * kWin);
+            if (gather == 2) {  // all gathers of the window first, then all stores
+                constexpr int K = (int)(kWin / 16 / T);
+                u32x4 g[K];
+#pragma unroll
+                for (int k = 0; k < K; ++k) {
+                    const uint32_t a = (x + k * 977u + threadIdx.x * 5u) & (T * 8 - 8);
+                    g[k] = u32x4{s_gat[a], s_gat[a + 1], s_gat[a + 2] ^ x, s_gat[a + 5]};
+                }
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int k = 0; k < K; ++k) {
+                    if (STORE)
+                        o[k * T + threadIdx.x] = g[k];
+                    else
+                        asm volatile("" ::"v"(g[k][0]), "v"(g[k][1]));
+                }
+                __syncthreads();
+                continue;
+            }
 #pragma unroll
             for (int k = 0; k < (int)(kWin / 16 / T); ++k) {
-                const u32x4 v = u32x4{x, (uint32_t)k, tile, 0u};
+                u32x4 v = u32x4{x, (uint32_t)k, tile, 0u};
+                if (gather) {  // store data gathered from LDS at data-dependent words, as the decode's chunks
+                    const uint32_t a = (x + k * 977u + threadIdx.x * 5u) & (T * 8 - 8);
+                    v = u32x4{s_gat[a], s_gat[a + 1], s_gat[a + 2] ^ x, s_gat[a + 5]};
+                }
                 if (STORE)
                     o[k * T + threadIdx.x] = v;
                 else
@@ -86,6 +126,8 @@ int main(int argc, char **argv)
 {
     const int spin = argc > 1 ? atoi(argv[1]) : 2000;
     const int reps = argc > 2 ? atoi(argv[2]) : 20;
+    const int gather = argc > 3 ? atoi(argv[3]) : 0;  // 1: store data gathered from LDS
+    const int gridstride = argc > 4 ? atoi(argv[4]) : 0;  // 1: tiles grid-stride instead of by ticket
     const uint64_t n = 1ull << 30;
     uint8_t *out;
     uint32_t *ticket;
@@ -114,16 +156,16 @@ int main(int argc, char **argv)
     };
     timeit("fill", [&] { hipLaunchKernelGGL(fill_kernel, dim3(cus * 8), dim3(256), 0, nullptr, (u32x4 *)out, n / 16); });
     timeit("tiles (no work)", [&] {
-        hipLaunchKernelGGL(tiles_kernel<true>, dim3(cus * 2), dim3(T), 0, nullptr, out, ntiles, ticket, 0);
+        hipLaunchKernelGGL(tiles_kernel<true>, dim3(cus * 2), dim3(T), 0, nullptr, out, ntiles, ticket, 0, gather, gridstride);
     });
     char name[64];
     snprintf(name, sizeof name, "tiles + work(%d)", spin);
     timeit(name, [&] {
-        hipLaunchKernelGGL(tiles_kernel<true>, dim3(cus * 2), dim3(T), 0, nullptr, out, ntiles, ticket, spin);
+        hipLaunchKernelGGL(tiles_kernel<true>, dim3(cus * 2), dim3(T), 0, nullptr, out, ntiles, ticket, spin, gather, gridstride);
     });
     snprintf(name, sizeof name, "work(%d) alone", spin);
     timeit(name, [&] {
-        hipLaunchKernelGGL(tiles_kernel<false>, dim3(cus * 2), dim3(T), 0, nullptr, out, ntiles, ticket, spin);
+        hipLaunchKernelGGL(tiles_kernel<false>, dim3(cus * 2), dim3(T), 0, nullptr, out, ntiles, ticket, spin, gather, gridstride);
     });
     CK(hipDeviceSynchronize());
     return 0;
