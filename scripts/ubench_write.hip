@@ -8,7 +8,7 @@
 //          each window's stores (the decode's marks and scan), barrier-separated
 //   work:  the phases alone, no stores (spin < 0: -spin LDS write+read round trips per phase instead of VALU; spin <= -1000: -(spin+1000) LDS reads only)
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 scripts/ubench_write.hip -o scripts/ubench_write.bin
-//   scripts/ubench_write.bin [spin=2000] [reps=20] [gather=0: 1 = store data read from LDS, 2 = all gathers then all stores] [gridstride=0]
+//   scripts/ubench_write.bin [spin=2000] [reps=20] [gather=0: 1 = store data read from LDS, 2 = all gathers then all stores, 3 = from ds_bpermute] [gridstride=0]
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -106,7 +106,12 @@ __global__ __launch_bounds__(T, 4) void tiles_kernel(uint8_t *out, uint32_t ntil
 #pragma unroll
             for (int k = 0; k < (int)(kWin / 16 / T); ++k) {
                 u32x4 v = u32x4{x, (uint32_t)k, tile, 0u};
-                if (gather) {  // store data gathered from LDS at data-dependent words, as the decode's chunks
+                if (gather == 3) {  // store data from other lanes by ds_bpermute (no LDS memory access)
+                    const int src = (int)(((x + k * 977u) & 63u) << 2);
+                    v = u32x4{(uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)x),
+                              (uint32_t)__builtin_amdgcn_ds_bpermute(src + 4, (int)(x ^ k)),
+                              (uint32_t)__builtin_amdgcn_ds_bpermute(src + 8, (int)tile), x};
+                } else if (gather) {  // store data gathered from LDS at data-dependent words, as the decode's chunks
                     const uint32_t a = (x + k * 977u + threadIdx.x * 5u) & (T * 8 - 8);
                     v = u32x4{s_gat[a], s_gat[a + 1], s_gat[a + 2] ^ x, s_gat[a + 5]};
                 }
