@@ -1645,6 +1645,52 @@ __global__ __launch_bounds__(kRoThreads, 4) void rl_offsets_kernel(  // 4 workgr
 constexpr int kPfxSlots = 256 + 3 * 7 + 1;
 __device__ __forceinline__ uint32_t pfx_slot(uint32_t x) { return x + 3u * (x >> 5); }
 
+// The run of chunk q's first byte and its inner start mask (first half of rd_chunk).
+__device__ __forceinline__ void rd_chunk_run(const uint32_t *bm, const uint32_t *pre, uint32_t q, uint32_t before,
+                                             int32_t &r_out, uint32_t &m1_out)
+{
+    const uint32_t word = bm[q >> 1];
+    const uint32_t m = (q & 1) ? word >> 16 : word & 0xFFFFu;
+    const uint32_t pq = pre[q >> 1] + ((q & 1) ? __popc(word & 0xFFFFu) : 0u);
+    int32_t r = (int32_t)(before + pq + (m & 1u)) - 1;
+    uint32_t m1 = m & 0xFFFEu;
+    if (r < 0) {
+        m1 &= m1 - 1;
+        r = 0;
+    }
+    r_out = r;
+    m1_out = m1;
+}
+
+// Second half of rd_chunk with the values taken from registers instead of LDS:
+// lane l of the wave holds values base4 + 4l .. base4 + 4l + 3 in `vreg`, and
+// the chunk's dwords come by ds_bpermute (the caller checks that every run the
+// wave's chunks need is in that range). Store data that passes through LDS
+// reads does not overlap other waves' LDS work (scripts/ubench_write.hip).
+__device__ __forceinline__ u32x4 rd_chunk_bp(uint32_t vreg, uint32_t base4, const uint64_t *pfx, int32_t r,
+                                             uint32_t m1)
+{
+    const uint32_t o = (uint32_t)r - base4, a = o >> 2, sh = o & 3u;
+    const uint32_t d0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(a << 2), (int)vreg);
+    const uint32_t d1 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((a + 1) << 2), (int)vreg);
+    const uint32_t d2 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((a + 2) << 2), (int)vreg);
+    const uint32_t o8 = o + (uint32_t)__popc(m1 & 0x1FFu), a8 = o8 >> 2, sh8 = o8 & 3u;
+    const uint32_t e0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(a8 << 2), (int)vreg);
+    const uint32_t e1 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((a8 + 1) << 2), (int)vreg);
+    const uint32_t e2 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((a8 + 2) << 2), (int)vreg);
+    const uint64_t klo = pfx[pfx_slot(m1 & 0xFFu)], khi = pfx[pfx_slot((m1 >> 8) & 0xFEu)];
+    const uint32_t w0 = __builtin_amdgcn_alignbyte(d1, d0, sh);
+    const uint32_t w1 = __builtin_amdgcn_alignbyte(d2, d1, sh);
+    const uint32_t u0 = __builtin_amdgcn_alignbyte(e1, e0, sh8);
+    const uint32_t u1 = __builtin_amdgcn_alignbyte(e2, e1, sh8);
+    u32x4 v;
+    v[0] = __builtin_amdgcn_perm(w1, w0, (uint32_t)klo);
+    v[1] = __builtin_amdgcn_perm(w1, w0, (uint32_t)(klo >> 32));
+    v[2] = __builtin_amdgcn_perm(u1, u0, (uint32_t)khi);
+    v[3] = __builtin_amdgcn_perm(u1, u0, (uint32_t)(khi >> 32));
+    return v;
+}
+
 __device__ __forceinline__ u32x4 rd_chunk(const uint32_t *bm, const uint32_t *pre, const uint32_t *v32,
                                           const uint64_t *pfx, uint32_t q, uint32_t before)
 {
@@ -1917,10 +1963,36 @@ __global__ __launch_bounds__(T, 4) void rl_decode_kernel(  // 2nd: waves per SIM
                 for (int k = 0; k < CPT; ++k) {
                     const uint32_t q = (uint32_t)(k * T + tid);
                     const uint32_t off = 16u * q;
+#if FLRL_RD_BPERM
+                    // the wave's 64 chunks (1 KiB) need runs r(lane 0) .. r(lane 63) + 9: when
+                    // they fit in 64 lanes x 4 values (sparse windows), the values come from
+                    // registers by ds_bpermute; q < CPT T keeps every lane's bitmap reads in
+                    // the window's arrays, so all lanes compute r before the window-end test
+                    int32_t r;
+                    uint32_t m1;
+                    rd_chunk_run(s_bm, s_pre, q, starts_before, r, m1);
+                    const uint32_t r_lo = (uint32_t)__builtin_amdgcn_readfirstlane(r);
+                    const uint32_t r_hi = (uint32_t)__builtin_amdgcn_readlane(r, kWave - 1);
+                    const uint32_t base4 = r_lo & ~3u;
+                    const bool bp = r_hi >= r_lo && r_hi - base4 <= 235u;  // wave-uniform
+                    // (assembled before the window-end test: a lane past the end still holds
+                    // values that the lanes before it read by ds_bpermute)
+                    u32x4 o_bp = u32x4{0u, 0u, 0u, 0u};
+                    if (bp) {
+                        const uint32_t vi = (base4 >> 2) + (uint32_t)lane;
+                        const uint32_t vreg =
+                            reinterpret_cast<const uint32_t *>(s_val4)[vi < (uint32_t)(kRdRuns / 4 + 4) ? vi : 0u];
+                        o_bp = rd_chunk_bp(vreg, base4, s_pfx, r, m1);
+                    }
+#endif
                     if (off >= wl)
                         break;
 #if FLRL_ABL_RD & 1  // timing-only ablation: no chunk assembly
                     const u32x4 o = u32x4{q, starts_before, 0u, 0u};
+#elif FLRL_RD_BPERM
+                    const u32x4 o = bp ? o_bp
+                                       : rd_chunk(s_bm, s_pre, reinterpret_cast<const uint32_t *>(s_val4), s_pfx, q,
+                                                  starts_before);
 #else
                     const u32x4 o = rd_chunk(s_bm, s_pre, reinterpret_cast<const uint32_t *>(s_val4), s_pfx, q,
                                              starts_before);

@@ -18,7 +18,7 @@
      defined(FLRL_RD_UNROLL) || defined(FLRL_HOST_WORKERS) || defined(FLRL_HOST_CHUNK) ||                \
      defined(FLRL_HOST_DIRECT) || defined(FLRL_HOST_PROFILE) || defined(FLRL_HOST_THP) || defined(FLRL_RL_WD64_MEAN) || defined(FLRL_RL_DENSE_MEAN) ||\
      defined(FLRL_RL_LAG) || defined(FLRL_RL_LAG_WPS) || defined(FLRL_RL_LAG_PER_CU) || defined(FLRL_RL_LAG_STAGE) || defined(FLRL_RL_LAG_GUARD) || defined(FLRL_RL_LAG_WAVES) || defined(FLRL_RL_LAG_EMIT) || defined(FLRL_RL_LAG_PF) ||\
-     defined(FLRL_FL_STORE_SPLIT) || defined(FLRL_FL_STORE_SKIP) || defined(FLRL_RL_SUB) || defined(FLRL_RL_FLUSH_NT) || defined(FLRL_RD_WAVE_NT) || defined(FLRL_ABL_FLUSH) || defined(FLRL_RL_DENSE_PF_EARLY) || defined(FLRL_ABL_RD))
+     defined(FLRL_FL_STORE_SPLIT) || defined(FLRL_FL_STORE_SKIP) || defined(FLRL_RL_SUB) || defined(FLRL_RL_FLUSH_NT) || defined(FLRL_RD_WAVE_NT) || defined(FLRL_ABL_FLUSH) || defined(FLRL_RL_DENSE_PF_EARLY) || defined(FLRL_ABL_RD) || defined(FLRL_RD_BPERM))
 #error "FLRL_* kernel overrides are for timing harnesses only (define FLRL_TUNING_BUILD)"
 #endif
 
@@ -60,6 +60,9 @@
 #endif
 #ifndef FLRL_ABL_RD
 #define FLRL_ABL_RD 0  // timing-only ablations of the RL block decode (1: no assembly, 2: no marks, 4: no stores, 8: whole-chunk stores only)
+#endif
+#ifndef FLRL_RD_BPERM
+#define FLRL_RD_BPERM 0  // RL block decode: sparse windows' chunk values by ds_bpermute from registers
 #endif
 #ifndef FLRL_FL_LOOKG
 #define FLRL_FL_LOOKG 1  // FL encode look-back granules per lane (window 64 G tiles)
