@@ -169,6 +169,35 @@ def cpu_baseline(kind: str, seed: int, sample: int, gpu_bits, gpu_values):
     }
 
 
+def rl_cpu_baseline(n: int, seed: int) -> dict:
+    """The RL oracle (1 core) on n bytes of runs32 (BASELINE configs[2]'s
+    input, the product generator): the rl-cpu figure for lines where the
+    GPU RL section does not run (N > 1)."""
+    import oracle
+    a = flrl.gen_host("runs32", n, seed)
+    t0 = time.perf_counter()
+    counts, values = oracle.rl_compress(a)
+    t1 = time.perf_counter()
+    back = oracle.rl_decompress(counts, values, n)
+    t2 = time.perf_counter()
+    return {"value": round(n / (t2 - t0) / 1e9, 4), "unit": "GB/s", "cores": 1, "kind": "port",
+            "sample": f"{n} bytes runs32 (seed {seed}); oracle rl encode {t1 - t0:.2f} s + decode {t2 - t1:.2f} s, "
+                      f"single-threaded",
+            "runs": int(counts.size), "roundtrip_ok": bool(np.array_equal(back, a))}
+
+
+def line_cpu_baseline(rank: int, world: int, kind: str, seed: int, sample: int, gpu_bits=None, gpu_values=None):
+    """The line's `cpu_baseline` (rank 0 only, any N; None when sample == 0):
+    the FL oracle on the first `sample` bytes of rank 0's shard, and at N > 1
+    the RL oracle as `rl` (at N = 1 the RL section carries its own)."""
+    if rank != 0 or sample <= 0:
+        return None
+    cpu = cpu_baseline(kind, seed, sample, gpu_bits, gpu_values)
+    if world > 1:
+        cpu["rl"] = rl_cpu_baseline(sample, seed)
+    return cpu
+
+
 def rank_shard(per_gpu: int, global_bytes: int, world: int, rank: int) -> tuple[int, int, int]:
     """(start, length, job total) of rank's input bytes. Weak scaling (the
     default): `per_gpu` bytes per rank, rank r at r * per_gpu. Strong scaling
@@ -632,9 +661,10 @@ def main():
     roundtrip = bool(torch.equal(out[:n], x[:n])) and err == 0
     parity = {"roundtrip": roundtrip, "device_error": err}
     gpu_bits = gpu_values = None
-    if rank == 0 and world == 1:
+    if rank == 0:  # (N > 1: rank 0's shard, for the CPU baseline's comparison)
         gpu_bits = codec.bits[: codec.frames].cpu().numpy()
         gpu_values = codec.values[:v].cpu().numpy()
+    if rank == 0 and world == 1:
         sha = file_sha(n, codec.frames, gpu_bits, gpu_values)
         parity["fl_sha256"] = sha
         if args.kind == "u8" and args.seed == 42 and n == 1 << 30:
@@ -747,21 +777,27 @@ def main():
                               n=args.configs4_bytes, rccl=rccl)
 
     if rank == 0:
-        cpu = None
+        # The CPU baseline runs on rank 0 at every N (north_star: "next to the
+        # reference fl-cpu/rl-cpu ... in the same run"), after the timed region,
+        # on the first min(n, 1 GiB) bytes of rank 0's shard (the shard starts
+        # at byte 0 in both scaling modes, so the oracle's generator gives the
+        # same bytes); at N > 1 it also times the RL oracle on runs32.
         sample = min(n, 1 << 30) if args.cpu_sample < 0 else args.cpu_sample
-        if world == 1 and sample > 0:
-            cpu = cpu_baseline(args.kind, args.seed, sample, gpu_bits, gpu_values)
+        cpu = line_cpu_baseline(rank, world, args.kind, args.seed, sample, gpu_bits, gpu_values)
+        del gpu_bits, gpu_values
         ns = None
         if world == 1 and not args.no_north_star and not (n == 16 << 30 and args.kind == "u8"):
             ns = north_star_section(args.seed, args.steps, args.warmup, dev)
-        c3 = None
-        if world == 1 and not args.no_configs3:
-            c3 = configs3_section(args.seed, args.steps, args.warmup, dev)
         rl = None
         if world == 1 and not args.no_rl:
             rl = rl_section(n, args.seed, args.steps, args.warmup, dev, cpu=sample > 0)
             if not args.no_rl_dense:
                 rl["dense_u8"] = rl_dense_section(n, args.seed, args.steps, args.warmup, dev)
+        # configs[3] last (16 + 1 GiB of lo4 buffers, released before it returns),
+        # so the sections above run with the same memory as without it
+        c3 = None
+        if world == 1 and not args.no_configs3:
+            c3 = configs3_section(args.seed, args.steps, args.warmup, dev)
         line = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -821,6 +857,8 @@ def main():
             "north_star": ns,
             "configs3": c3,
             "configs4": c4,
+            "sections_run": {"cpu_baseline": cpu is not None, "north_star": ns is not None, "rl": rl is not None,
+                             "configs3": c3 is not None, "configs4": c4 is not None},
         }
         print(json.dumps(line), flush=True)
     if comm is not None:

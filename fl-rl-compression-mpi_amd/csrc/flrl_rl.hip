@@ -51,13 +51,6 @@ constexpr int kRlThreads = FLRL_RL_THREADS;         // encode workgroup: 4 waves
 constexpr int kRlLaneBytes = 64;                    // contiguous bytes per lane (a u64 head mask)
 constexpr int kRlSub = FLRL_RL_SUB;                 // sub-chunks of 4 KiB per wave chunk (one look-back per tile)
 constexpr int kRlTileBytes = kRlLaneBytes * kRlThreads * kRlSub;  // 128 KiB: 4 waves x 32 KiB
-// persistent form (rl_encode_lag_kernel): FLRL_RL_LAG_WAVES data waves of 32 KiB
-// chunks + the look-back wave per workgroup
-constexpr int kRlLagWaves = FLRL_RL_LAG_WAVES;
-constexpr int kRlLagThreads = kWave * (kRlLagWaves + 1);
-constexpr int kRlLagTileBytes = kRlLaneBytes * kWave * kRlSub * kRlLagWaves;
-constexpr int kRlEncTileBytes = FLRL_RL_LAG ? kRlLagTileBytes : kRlTileBytes;  // tiles of the shipped form
-static_assert((uint64_t)kWave * FLRL_RL_LOOKG * kRlLagTileBytes < (1ull << 26), "look-back window maps within the 26-bit fields");
 constexpr int kRlLookG = FLRL_RL_LOOKG;  // look-back granules per lane (window 64 G tiles)
 constexpr int kRlLookL = FLRL_RL_LOOKL;  // look-back lanes polled per window
 constexpr int kRlStatusStride = FLRL_RL_STATUS_STRIDE;  // status granules per tile
@@ -404,54 +397,6 @@ __device__ __forceinline__ void store_chunk_part(uint8_t *dst, u32x4 v, uint32_t
         dst[a] = (uint8_t)(dw(a) >> (8 * (a & 3)));
 }
 
-// Bytes [A, A + cnt) of dst = src[s0 .. s0 + cnt) (src in LDS, 4-byte aligned,
-// readable 20 bytes past its end), by one wave: a 16-byte store per lane for
-// every aligned chunk inside the range, naturally aligned 1/2/4/8-byte pieces
-// for the two chunks it shares with its neighbours (written by their owners).
-__device__ __forceinline__ void lds_flush(uint8_t *__restrict__ dst, uint64_t A, uint32_t cnt, const uint8_t *src,
-                                          uint32_t s0, int lane)
-{
-    const uint32_t a = (uint32_t)(A & 15u);
-    const uint32_t span = a + cnt;
-    uint8_t *const base = dst + (A - a);
-    const uint32_t *const s32 = reinterpret_cast<const uint32_t *>(src);
-    for (uint32_t q = (uint32_t)lane; cnt && 16 * q < span; q += kWave) {
-        const int32_t o = (int32_t)(16 * q) - (int32_t)a + (int32_t)s0;  // src index of the chunk's byte 0
-        const int32_t d = o >> 2;  // arithmetic: floor
-        const uint32_t sh = (uint32_t)o & 3u;
-        uint32_t wd[5];
-#pragma unroll
-        for (int i = 0; i < 5; ++i)
-            wd[i] = d + i < 0 ? 0u : s32[d + i];
-        const u32x4 v = u32x4{__builtin_amdgcn_alignbyte(wd[1], wd[0], sh), __builtin_amdgcn_alignbyte(wd[2], wd[1], sh),
-                              __builtin_amdgcn_alignbyte(wd[3], wd[2], sh), __builtin_amdgcn_alignbyte(wd[4], wd[3], sh)};
-        const uint32_t lo = q == 0 ? a : 0u;
-        const uint32_t hi = span - 16 * q < 16 ? span - 16 * q : 16u;
-        if (lo == 0 && hi == 16)
-            *reinterpret_cast<u32x4 *>(base + 16 * q) = v;
-        else
-            store_chunk_part(base + 16 * q, v, lo, hi);
-    }
-}
-
-// Bytes [A, A + cnt) of dst = the byte x, as lds_flush stores them.
-__device__ __forceinline__ void byte_fill(uint8_t *__restrict__ dst, uint64_t A, uint32_t cnt, uint32_t x, int lane)
-{
-    const uint32_t a = (uint32_t)(A & 15u);
-    const uint32_t span = a + cnt;
-    uint8_t *const base = dst + (A - a);
-    const uint32_t x4 = (x & 0xFFu) * 0x01010101u;
-    const u32x4 v = u32x4{x4, x4, x4, x4};
-    for (uint32_t q = (uint32_t)lane; cnt && 16 * q < span; q += kWave) {
-        const uint32_t lo = q == 0 ? a : 0u;
-        const uint32_t hi = span - 16 * q < 16 ? span - 16 * q : 16u;
-        if (lo == 0 && hi == 16)
-            *reinterpret_cast<u32x4 *>(base + 16 * q) = v;
-        else
-            store_chunk_part(base + 16 * q, v, lo, hi);
-    }
-}
-
 // Wave-uniform values held in scalar registers (the compiler cannot prove
 // that values read from LDS or derived from the wave index are uniform).
 __device__ __forceinline__ uint32_t uniform32(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
@@ -497,7 +442,7 @@ struct RlWave {
     // LDS per workgroup: W images and the run staging
     static constexpr int kLdsBytes = W * WB + STG;
     static_assert(LB == 64, "one u64 head mask per lane (piece emission: 4 x 16 positions)");
-    static_assert(TBT == kRlTileBytes || TBT == kRlLagTileBytes, "tile geometry shared with the layout");
+    static_assert(TBT == kRlTileBytes, "tile geometry shared with the layout");
 
     struct Sub {
         uint32_t nat[CH / 2];  // 16-bit natural-head masks, two per word
@@ -791,22 +736,10 @@ struct RlWave {
             const uint32_t hi = span - 16 * q < 16 ? span - 16 * q : 16u;
 #pragma unroll
             for (int arr = 0; arr < 2; ++arr) {
-#if FLRL_ABL_FLUSH == 1  // timing-only ablation: no LDS gather
-                const u32x4 v = u32x4{(uint32_t)o, 1u, 2u, 3u};
-#else
                 const u32x4 v = piece_gather(arr ? stv : stc, o);
-#endif
                 uint8_t *const d = (arr ? pv : pc) + 16 * q;
-#if FLRL_ABL_FLUSH == 2  // timing-only ablation: no stores
-                asm volatile("" ::"v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]));
-                continue;
-#endif
                 if (lo == 0 && hi == 16) {
-#if FLRL_RL_FLUSH_NT
-                    __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(d));
-#else
-                    *reinterpret_cast<u32x4 *>(d) = v;
-#endif
+                    *reinterpret_cast<u32x4 *>(d) = v;  // (non-temporal: +-0.2 %)
                 } else {
                     store_chunk_part(d, v, lo, hi);
                 }
@@ -946,10 +879,6 @@ struct RlWave {
                 // four parts of 16 rows (<= 1024 records each, within the staging),
                 // each staged by piece_part and stored with 16-byte stores
                 const uint32_t sl = (uint32_t)(g - hb);
-#if FLRL_RL_DENSE_PF_EARLY
-                if (s + 1 < ns)
-                    load_sub(off, s + 1, pf);  // in flight across the pieces' stores
-#endif
 #pragma unroll 1
                 for (int p = 0; p < kWave / 16; ++p) {
                     const uint32_t b0 = (uint32_t)__builtin_amdgcn_readlane((int)sl, 16 * p);
@@ -960,7 +889,7 @@ struct RlWave {
                     wave_lds_sync();
                 }
             }
-            if (!FLRL_RL_DENSE_PF_EARLY && hs > (uint32_t)SW && s + 1 < ns)
+            if (hs > (uint32_t)SW && s + 1 < ns)
                 load_sub(off, s + 1, pf);  // after the pieces: see above
             hb += hs;
             rel = pm_compose(rel, L.smap);
@@ -1162,329 +1091,6 @@ __global__ __launch_bounds__(T, kRlWavesPerSimd) void rl_encode_wave_kernel(  //
         raise_error(ctrl, FLRL_E_ARG);
 }
 
-// ---- persistent RL encode: a look-back wave one tile behind the scan --------
-// FLRL_RL_LAG_GUARD (timing harnesses only): the look-back wave's stores are
-// bounds-checked; a violation skips the store and raises 90 + site with the
-// tile in Ctrl::aux (a fault probe, never in a shipped build).
-#ifdef FLRL_RL_LAG_GUARD
-#define RL_LAG_GUARD(ok, site, ctrl, tile)                                                  \
-    if (!(ok)) {                                                                            \
-        if ((threadIdx.x & 63) == 0) {                                                      \
-            atomicCAS(&(ctrl)->error, 0u, 90u + (site));                                    \
-            (ctrl)->aux = ((uint64_t)(tile) << 8) | (site);                                 \
-        }                                                                                   \
-        continue;                                                                           \
-    }
-#else
-#define RL_LAG_GUARD(ok, site, ctrl, tile)
-#endif
-
-// Pointers into LDS and global memory typed with their address space at the
-// helpers' boundaries (once out-of-line calls: with plain pointers a callee saw
-// generic ones, every access became a flat instruction, and the build faulted
-// on the GPU with an aperture violation; inlined now, the types keep the
-// helpers' accesses ds_ / global_ whatever the caller's pointer provenance).
-typedef __attribute__((address_space(3))) uint8_t lds_u8;
-typedef __attribute__((address_space(3))) uint64_t lds_u64;
-typedef __attribute__((address_space(1))) uint8_t glb_u8;
-typedef __attribute__((address_space(1))) uint64_t glb_u64;
-template <class T>
-__device__ __forceinline__ lds_u8 *as_lds(T *p) { return (lds_u8 *)(p); }
-__device__ __forceinline__ glb_u8 *as_glb(uint8_t *p) { return (glb_u8 *)(p); }
-__device__ __forceinline__ glb_u64 *as_glb(uint64_t *p) { return (glb_u64 *)(p); }
-
-// What the look-back wave needs of a data wave's chunk to emit it (LDS).
-struct RlChunkInfo {
-    uint32_t first;   // first natural head (chunk-relative; kNone: none)
-    uint32_t K;       // state-independent heads (all staged unless overflowed)
-    uint32_t rel_in;  // PhaseMap over the chunk
-    uint32_t v0;      // the chunk's first byte; bit 8: the staging overflowed
-    uint32_t nst, Kst, rel_st, pad;  // the rest of the Chunk (overflowed tiles)
-};
-constexpr uint32_t kRlOverflow = 0x100u;
-
-// Emission of chunk v of a tile whose runs are all staged (sc: that chunk's
-// staging slice, counts then values), with the chunk's state st (heads before
-// it, chunk state at its start), by one wave: its split heads (255, v0), the
-// run of its first natural head (count from the incoming state) and the
-// staged runs, as 16-byte stores; the final run if the chunk ends the input.
-template <class Wv>
-__device__ __forceinline__ void rl_emit_staged_chunk(const uint8_t *__restrict__ in, uint64_t n, uint8_t *sc,
-                                                     const RlChunkInfo &info, uint32_t tile, int v, uint64_t st,
-                                                     uint8_t *__restrict__ counts, uint8_t *__restrict__ values,
-                                                     uint64_t *__restrict__ runs_out, Ctrl *ctrl)
-{
-    int lane = threadIdx.x & (kWave - 1);
-    asm volatile("" : "+v"(lane));  // lane-derived addresses stay inside the caller's loop iteration
-    const uint64_t off = (uint64_t)tile * Wv::TBT + (uint64_t)v * Wv::CB;
-    if (off >= n)
-        return;
-    do {
-        RL_LAG_GUARD(sm_h(st) <= n && (st & kSmKind) == kSmConst, 0, ctrl, tile)
-        const uint32_t len = n - off < (uint64_t)Wv::CB ? (uint32_t)(n - off) : (uint32_t)Wv::CB;
-        const uint32_t first = uniform32(info.first), K = uniform32(info.K);
-        const uint32_t rel_in = uniform32(info.rel_in), v0 = uniform32(info.v0) & 0xFFu;
-        const uint64_t h_in = uniform64(sm_h(st));
-        const uint32_t c_in = uniform32(sm_c(st));
-        const uint32_t pre = first != Wv::kNone ? first : len;
-        const uint32_t S = splits(c_in, pre);
-        RL_LAG_GUARD(K <= Wv::SW && S <= 130 && h_in + S + K <= n, 1, ctrl, tile)
-        // split heads h_in + j (j < S) end 255-byte pieces of v0; record g is
-        // output byte g - 1 (record 0, the input's first head, ends no run)
-        {
-            const uint64_t g = h_in == 0 ? 1 : h_in, e = h_in + S;
-            if (e > g) {
-                byte_fill(counts, g - 1, (uint32_t)(e - g), 255u, lane);
-                byte_fill(values, g - 1, (uint32_t)(e - g), v0, lane);
-            }
-        }
-        const uint64_t g0 = h_in + S;  // record of the first natural head
-        if (K) {
-            uint8_t *const sv = sc + Wv::SW;
-            if (lane == 0) {
-                const uint32_t c = add_c(c_in, first);
-                sc[0] = (uint8_t)(c == 0 ? 255u : c);
-            }
-            wave_lds_sync();
-            const uint32_t j0 = g0 == 0 ? 1u : 0u;
-            lds_flush(counts, g0 + j0 - 1, K - j0, sc, j0, lane);
-            lds_flush(values, g0 + j0 - 1, K - j0, sv, j0, lane);
-        }
-        if (off + len == n && lane == 0) {  // the final run (ends at byte n-1)
-            const uint64_t R = g0 + K;
-            const uint32_t c_end = pm_apply(rel_in, c_in);
-            counts[R - 1] = (uint8_t)(c_end == 0 ? 255u : c_end);
-            values[R - 1] = in[n - 1];
-            *runs_out = R;
-        }
-    } while (false);
-}
-
-// The look-back wave's part of a tile (persistent form): publish the tile's
-// map, resolve its state, then either emit its staged runs itself
-// (FLRL_RL_LAG_EMIT 0) or hand every chunk's state to the data waves (s_st:
-// always for a tile whose staging overflowed, as its data waves re-read it).
-// Inlined into the look-back wave's own loop: the kernel must use no scratch
-// at all (a call's saved registers live there, and a kernel with scratch got
-// fewer workgroups per CU than its persistent grid, see below).
-template <class Wv, int W>
-__device__ __forceinline__ void rl_lag_resolve(const glb_u8 *in_g, uint64_t n, lds_u8 *stg_l, lds_u8 *info_l,
-                                               lds_u8 *maps_l, lds_u8 *st_l, bool ovf, uint32_t tile,
-                                               glb_u8 *counts_g, glb_u8 *values_g, glb_u64 *runs_g, glb_u8 *ctrl_g,
-                                               glb_u64 *status_g, uint64_t help_ticks)
-{
-    const uint8_t *const in = (const uint8_t *)in_g;
-    uint8_t *const stg = (uint8_t *)stg_l;
-    const RlChunkInfo *const info = (const RlChunkInfo *)(uint8_t *)info_l;
-    const uint64_t *const maps = (const uint64_t *)(uint8_t *)maps_l;
-    uint64_t *const s_st = (uint64_t *)(uint8_t *)st_l;
-    Ctrl *const ctrl = (Ctrl *)(uint8_t *)ctrl_g;
-    uint64_t *const status = (uint64_t *)status_g;
-    uint64_t tmap = maps[0];
-#pragma unroll
-    for (int v = 1; v < W; ++v)
-        tmap = sm_compose(tmap, maps[v]);
-    publish_seg<kRlStatusStride>(status, tile, tmap);
-    FLRL_RL_TRACE(tile, 2);
-    auto help = [&](uint32_t t) -> uint64_t { return rl_tile_map_slow<Wv::TBT>(in, n, t); };
-    uint64_t st = lookback_seg<kRlLookG, kRlLookL, kRlStatusStride>(status, tile, tmap, ctrl, help_ticks, help);
-    FLRL_RL_TRACE(tile, 3);
-    if (FLRL_RL_LAG_EMIT || ovf) {
-        if ((threadIdx.x & (kWave - 1)) == 0) {
-#pragma unroll
-            for (int v = 0; v < W; ++v) {
-                s_st[v] = st;
-                st = sm_compose(st, maps[v]);
-            }
-        }
-    } else {
-        uint8_t *const counts = (uint8_t *)counts_g;
-        uint8_t *const values = (uint8_t *)values_g;
-        uint64_t *const runs_out = (uint64_t *)runs_g;
-#pragma unroll 1
-        for (int v = 0; v < W; ++v) {
-            rl_emit_staged_chunk<Wv>(in, n, stg + v * 2 * Wv::SW, info[v], tile, v, st, counts, values, runs_out,
-                                     ctrl);
-            st = sm_compose(st, maps[v]);
-        }
-        FLRL_RL_TRACE(tile, 4);
-    }
-}
-
-// Persistent form: one workgroup per slot (FLRL_RL_LAG_PER_CU per CU), W data
-// waves + one look-back wave. The data waves scan tile i's chunks into staging
-// buffer i mod 2 and leave its maps and chunk facts in LDS; ONE barrier per
-// tile; then they go straight on to tile i+1 while the look-back wave
-// publishes tile i and resolves its state (and takes the ticket of tile i+2).
-// Tile i's staged runs leave either by the look-back wave (FLRL_RL_LAG_EMIT 0)
-// or by the data waves at the top of their next tile, each its own chunk
-// (FLRL_RL_LAG_EMIT 1: the look-back wave then issues no stores, so its
-// atomics and polls never wait for stores to drain). A tile whose staging
-// overflowed (dense runs: sub-chunks to re-read with the true states) is
-// emitted by its data waves as in rl_encode_wave_kernel, after a second
-// barrier at which the look-back wave hands over the states. The first tile of
-// a workgroup is its index, the rest by ticket.
-template <int W, int LB, int SUB, int STG>
-__global__ __launch_bounds__(kWave * (W + 1), FLRL_RL_LAG_WPS) void rl_encode_lag_kernel(
-    const uint8_t *__restrict__ in, uint64_t n, uint32_t ntiles, uint8_t *__restrict__ counts,
-    uint8_t *__restrict__ values, uint64_t *__restrict__ runs_out, Ctrl *ctrl, uint64_t *status,
-    uint64_t help_ticks)
-{
-    using Wv = RlWave<LB, SUB, W, STG, FLRL_RL_LAG_PF>;
-    constexpr int kStg = STG + 32;  // + the flush's read slack
-    constexpr bool kDataEmit = FLRL_RL_LAG_EMIT != 0;
-    __shared__ __attribute__((aligned(16))) uint8_t s_img[W * Wv::WB];
-    __shared__ __attribute__((aligned(16))) uint8_t s_stg[2][kStg];
-    __shared__ uint64_t s_map[2][W];
-    __shared__ RlChunkInfo s_info[2][W];
-    __shared__ uint64_t s_st[2][W];
-    __shared__ uint32_t s_tile[2];
-    __shared__ uint32_t s_prev[2][W];
-    // the arguments only the emission paths need, parked in LDS: re-read after
-    // each barrier, they hold no scalar registers across the scan loop
-    struct Args {
-        uint8_t *counts, *values;
-        uint64_t *runs_out, *status;
-        Ctrl *ctrl;
-        uint64_t help_ticks;
-    };
-    __shared__ Args s_args;
-
-    const int tid = threadIdx.x;
-    const int w = __builtin_amdgcn_readfirstlane(tid / kWave);
-    const bool lw = w == W;  // the look-back wave
-    Wv V(in, n, s_img, lw ? 0 : w);
-    uint32_t tile = blockIdx.x;
-    if (tile >= ntiles)
-        return;
-    if (tid == 0)
-        s_args = Args{counts, values, runs_out, status, ctrl, help_ticks};
-    // a tile ticket: tiles from gridDim.x on. A launch draws exactly ntiles
-    // tickets (each workgroup until its first past the end), so a raw ticket
-    // >= ntiles means the scratch's counter was not reset for this launch.
-    auto ticket = [&](Ctrl *c) -> uint32_t {
-        const uint32_t raw = atomicAdd(&c->ticket, 1u);
-        if (raw >= ntiles) {
-            raise_error(c, FLRL_E_ARG);
-            return ntiles;
-        }
-        const uint64_t t = (uint64_t)raw + gridDim.x;
-        return t < ntiles ? (uint32_t)t : ntiles;
-    };
-    if (lw && V.lane == 0)
-        s_tile[1] = ticket(ctrl);
-    auto scan = [&](uint32_t t, int b) {
-        V.relane();
-        V.stage_at(s_stg[b]);
-        const uint64_t off = (uint64_t)t * Wv::TBT + (uint64_t)w * Wv::CB;
-        typename Wv::Chunk C;
-        V.scan_chunk(off, off >= n ? 0u : (n - off < (uint64_t)Wv::CB ? (uint32_t)(n - off) : (uint32_t)Wv::CB), C);
-        if (V.lane == 0) {
-            s_map[b][w] = C.map();
-            s_info[b][w] = RlChunkInfo{C.first, C.K, C.rel_in, C.v0 | (C.nst < C.ns ? kRlOverflow : 0u),
-                                       (uint32_t)C.nst, C.Kst, C.rel_st, 0u};
-        }
-    };
-    auto tile_overflowed = [&](int b) {
-        bool ovf = false;
-#pragma unroll
-        for (int v = 0; v < W; ++v)
-            ovf |= (s_info[b][v].v0 & kRlOverflow) != 0;
-        return ovf;
-    };
-    FLRL_RL_TRACE(tile, 0);
-    // The two roles run separate loops with the same barrier sequence per tile
-    // (A: the tile is scanned; B, only when a chunk's staging overflowed: the
-    // states are in s_st; with FLRL_RL_LAG_EMIT 1 and a last tile that did not
-    // overflow, one more at the end: its states), so each loop's registers are
-    // allocated on their own: one loop holding both roles' live values spilled
-    // to scratch, and a kernel with scratch is dispatched with fewer
-    // workgroups per CU than the persistent grid assumes.
-    if (!lw) {
-        // the data waves' emission of their own chunk of a staged tile
-        auto emit_staged = [&](uint32_t t, int b) {
-            const Args a = s_args;
-            rl_emit_staged_chunk<Wv>(in, n, s_stg[b] + w * 2 * Wv::SW, s_info[b][w], t, w, s_st[b][w], a.counts,
-                                     a.values, a.runs_out, a.ctrl);
-        };
-        // s_prev[x][w]: the tile in staging x whose staged runs this wave still
-        // has to emit (kNone: none), kept in LDS rather than in registers
-        if (V.lane == 0)
-            s_prev[1][w] = Wv::kNone;
-        scan(tile, 0);
-        int b = 0;
-        for (;;) {
-            __syncthreads();  // A: tile scanned into staging b; s_tile[b ^ 1] = the next tile
-            const uint32_t nxt = s_tile[b ^ 1];
-            const bool ovf = tile_overflowed(b);
-            if (kDataEmit) {  // the previous tile (staging b ^ 1; its states came before A), if staged
-                const uint32_t prev = uniform32(s_prev[b ^ 1][w]);
-                if (prev != Wv::kNone)
-                    emit_staged(prev, b ^ 1);
-                if (V.lane == 0)
-                    s_prev[b][w] = ovf ? Wv::kNone : tile;
-            }
-            if (ovf) {
-                __syncthreads();  // B: the chunks' states in s_st[b]
-                // the chunk's facts back from LDS (nothing of the scan is live
-                // across the loop), then the emission of rl_encode_wave_kernel
-                const Args a = s_args;
-                const RlChunkInfo &I = s_info[b][w];
-                typename Wv::Chunk C;
-                C.off = (uint64_t)tile * Wv::TBT + (uint64_t)w * Wv::CB;
-                C.len = C.off >= n ? 0u : (n - C.off < (uint64_t)Wv::CB ? (uint32_t)(n - C.off) : (uint32_t)Wv::CB);
-                C.ns = (int)((C.len + Wv::WB - 1) / Wv::WB);
-                C.nst = (int)uniform32(I.nst);
-                C.first = uniform32(I.first);
-                C.K = uniform32(I.K);
-                C.Kst = uniform32(I.Kst);
-                C.rel_in = uniform32(I.rel_in);
-                C.rel_st = uniform32(I.rel_st);
-                C.v0 = uniform32(I.v0) & 0xFFu;
-                const uint64_t st = s_st[b][w];
-                V.relane();
-                V.stage_at(s_stg[b]);
-                V.emit(C, sm_h(st), sm_c(st), a.counts, a.values, a.runs_out);
-            }
-            if (nxt >= ntiles) {
-                if (kDataEmit && !ovf) {
-                    __syncthreads();  // C: the last tile's states in s_st[b]
-                    emit_staged(tile, b);
-                }
-                break;
-            }
-            FLRL_RL_TRACE(nxt, 0);
-            scan(nxt, b ^ 1);
-            tile = nxt;
-            b ^= 1;
-        }
-    } else {
-        int b = 0;
-        for (;;) {
-            __syncthreads();  // A
-            FLRL_RL_TRACE(tile, 1);
-            const uint32_t nxt = s_tile[b ^ 1];
-            const bool ovf = tile_overflowed(b);
-            // s_tile[b] was last read before barrier A
-            const Args a = s_args;
-            if (nxt < ntiles && V.lane == 0)
-                s_tile[b] = ticket(a.ctrl);
-            rl_lag_resolve<Wv, W>((const glb_u8 *)in, n, as_lds(s_stg[b]), as_lds(s_info[b]), as_lds(s_map[b]),
-                                  as_lds(s_st[b]), ovf, tile, as_glb(a.counts), as_glb(a.values), as_glb(a.runs_out),
-                                  (glb_u8 *)a.ctrl, as_glb(a.status), a.help_ticks);
-            if (ovf)
-                __syncthreads();  // B
-            if (nxt >= ntiles) {
-                if (kDataEmit && !ovf)
-                    __syncthreads();  // C
-                break;
-            }
-            tile = nxt;
-            b ^= 1;
-        }
-    }
-}
-
 // ---- decode pre-pass: output offsets of each decode tile ------------------
 // A workgroup (4 waves) takes a contiguous span of iters x kRoRuns counts by
 // ticket; wave w owns the w-th quarter of it and walks it in steps of 16384
@@ -1644,52 +1250,6 @@ __global__ __launch_bounds__(kRoThreads, 4) void rl_offsets_kernel(  // 4 workgr
 // entries spread the single-bit entries over distinct banks (~2.2).
 constexpr int kPfxSlots = 256 + 3 * 7 + 1;
 __device__ __forceinline__ uint32_t pfx_slot(uint32_t x) { return x + 3u * (x >> 5); }
-
-// The run of chunk q's first byte and its inner start mask (first half of rd_chunk).
-__device__ __forceinline__ void rd_chunk_run(const uint32_t *bm, const uint32_t *pre, uint32_t q, uint32_t before,
-                                             int32_t &r_out, uint32_t &m1_out)
-{
-    const uint32_t word = bm[q >> 1];
-    const uint32_t m = (q & 1) ? word >> 16 : word & 0xFFFFu;
-    const uint32_t pq = pre[q >> 1] + ((q & 1) ? __popc(word & 0xFFFFu) : 0u);
-    int32_t r = (int32_t)(before + pq + (m & 1u)) - 1;
-    uint32_t m1 = m & 0xFFFEu;
-    if (r < 0) {
-        m1 &= m1 - 1;
-        r = 0;
-    }
-    r_out = r;
-    m1_out = m1;
-}
-
-// Second half of rd_chunk with the values taken from registers instead of LDS:
-// lane l of the wave holds values base4 + 4l .. base4 + 4l + 3 in `vreg`, and
-// the chunk's dwords come by ds_bpermute (the caller checks that every run the
-// wave's chunks need is in that range). Store data that passes through LDS
-// reads does not overlap other waves' LDS work (scripts/ubench_write.hip).
-__device__ __forceinline__ u32x4 rd_chunk_bp(uint32_t vreg, uint32_t base4, const uint64_t *pfx, int32_t r,
-                                             uint32_t m1)
-{
-    const uint32_t o = (uint32_t)r - base4, a = o >> 2, sh = o & 3u;
-    const uint32_t d0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(a << 2), (int)vreg);
-    const uint32_t d1 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((a + 1) << 2), (int)vreg);
-    const uint32_t d2 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((a + 2) << 2), (int)vreg);
-    const uint32_t o8 = o + (uint32_t)__popc(m1 & 0x1FFu), a8 = o8 >> 2, sh8 = o8 & 3u;
-    const uint32_t e0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(a8 << 2), (int)vreg);
-    const uint32_t e1 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((a8 + 1) << 2), (int)vreg);
-    const uint32_t e2 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((a8 + 2) << 2), (int)vreg);
-    const uint64_t klo = pfx[pfx_slot(m1 & 0xFFu)], khi = pfx[pfx_slot((m1 >> 8) & 0xFEu)];
-    const uint32_t w0 = __builtin_amdgcn_alignbyte(d1, d0, sh);
-    const uint32_t w1 = __builtin_amdgcn_alignbyte(d2, d1, sh);
-    const uint32_t u0 = __builtin_amdgcn_alignbyte(e1, e0, sh8);
-    const uint32_t u1 = __builtin_amdgcn_alignbyte(e2, e1, sh8);
-    u32x4 v;
-    v[0] = __builtin_amdgcn_perm(w1, w0, (uint32_t)klo);
-    v[1] = __builtin_amdgcn_perm(w1, w0, (uint32_t)(klo >> 32));
-    v[2] = __builtin_amdgcn_perm(u1, u0, (uint32_t)khi);
-    v[3] = __builtin_amdgcn_perm(u1, u0, (uint32_t)(khi >> 32));
-    return v;
-}
 
 __device__ __forceinline__ u32x4 rd_chunk(const uint32_t *bm, const uint32_t *pre, const uint32_t *v32,
                                           const uint64_t *pfx, uint32_t q, uint32_t before)
@@ -1914,12 +1474,8 @@ __global__ __launch_bounds__(T, 4) void rl_decode_kernel(  // 2nd: waves per SIM
                         const int32_t x = tb + (int32_t)x0;
                         if (x >= kRkWindow)
                             break;
-#if FLRL_ABL_RD & 2  // timing-only ablation: no start marks
-                        asm volatile("" ::"v"(x), "v"(x1));
-#else
                         if (x1 > x0 && x >= 0)
                             atomicOr(&s_bm[(uint32_t)x >> 5], 1u << (x & 31));
-#endif
                     }
                 }
                 __syncthreads();
@@ -1963,48 +1519,10 @@ __global__ __launch_bounds__(T, 4) void rl_decode_kernel(  // 2nd: waves per SIM
                 for (int k = 0; k < CPT; ++k) {
                     const uint32_t q = (uint32_t)(k * T + tid);
                     const uint32_t off = 16u * q;
-#if FLRL_RD_BPERM
-                    // the wave's 64 chunks (1 KiB) need runs r(lane 0) .. r(lane 63) + 9: when
-                    // they fit in 64 lanes x 4 values (sparse windows), the values come from
-                    // registers by ds_bpermute; q < CPT T keeps every lane's bitmap reads in
-                    // the window's arrays, so all lanes compute r before the window-end test
-                    int32_t r;
-                    uint32_t m1;
-                    rd_chunk_run(s_bm, s_pre, q, starts_before, r, m1);
-                    const uint32_t r_lo = (uint32_t)__builtin_amdgcn_readfirstlane(r);
-                    const uint32_t r_hi = (uint32_t)__builtin_amdgcn_readlane(r, kWave - 1);
-                    const uint32_t base4 = r_lo & ~3u;
-                    const bool bp = r_hi >= r_lo && r_hi - base4 <= 235u;  // wave-uniform
-                    // (assembled before the window-end test: a lane past the end still holds
-                    // values that the lanes before it read by ds_bpermute)
-                    u32x4 o_bp = u32x4{0u, 0u, 0u, 0u};
-                    if (bp) {
-                        const uint32_t vi = (base4 >> 2) + (uint32_t)lane;
-                        const uint32_t vreg =
-                            reinterpret_cast<const uint32_t *>(s_val4)[vi < (uint32_t)(kRdRuns / 4 + 4) ? vi : 0u];
-                        o_bp = rd_chunk_bp(vreg, base4, s_pfx, r, m1);
-                    }
-#endif
                     if (off >= wl)
                         break;
-#if FLRL_ABL_RD & 1  // timing-only ablation: no chunk assembly
-                    const u32x4 o = u32x4{q, starts_before, 0u, 0u};
-#elif FLRL_RD_BPERM
-                    const u32x4 o = bp ? o_bp
-                                       : rd_chunk(s_bm, s_pre, reinterpret_cast<const uint32_t *>(s_val4), s_pfx, q,
-                                                  starts_before);
-#else
                     const u32x4 o = rd_chunk(s_bm, s_pre, reinterpret_cast<const uint32_t *>(s_val4), s_pfx, q,
                                              starts_before);
-#endif
-#if FLRL_ABL_RD & 4  // timing-only ablation: no output stores
-                    asm volatile("" ::"v"(o[0]), "v"(o[1]), "v"(o[2]), "v"(o[3]));
-                    continue;
-#endif
-#if FLRL_ABL_RD & 8  // timing-only ablation: every chunk stored whole (no edge path)
-                    *reinterpret_cast<u32x4 *>(outw + off) = o;
-                    continue;
-#endif
                     if (off >= b0 && off + 16 <= ce) {
                         *reinterpret_cast<u32x4 *>(outw + off) = o;  // plain: see the note above
                     } else {  // a chunk shared with a neighbouring tile: its bytes only
@@ -2199,11 +1717,7 @@ __global__ __launch_bounds__(kWdThreads) void rl_decode_wave_kernel(
                     const uint32_t lo = gq < b0 ? b0 - gq : 0u;
                     const uint32_t hi = gq + 16 > len ? len - gq : 16u;
                     if (lo == 0 && hi == 16)
-#if FLRL_RD_WAVE_NT
-                        __builtin_nontemporal_store(ov, reinterpret_cast<u32x4 *>(out + g0 + gq));
-#else
-                        *reinterpret_cast<u32x4 *>(out + g0 + gq) = ov;  // plain stores, as the block decode
-#endif
+                        *reinterpret_cast<u32x4 *>(out + g0 + gq) = ov;  // plain stores, as the block decode (nt: +4..17 %)
                     else  // a chunk shared with a neighbouring tile: its bytes only
                         store_chunk_part(out + g0 + gq, ov, lo, hi);
                 }
@@ -2222,7 +1736,7 @@ struct RlEncLayout {
     size_t tiles, zero, bytes;
     explicit RlEncLayout(size_t n)
     {
-        tiles = div_up(n, (size_t)kRlEncTileBytes);
+        tiles = div_up(n, (size_t)kRlTileBytes);
         zero = kRlStatusOff + round_up(tiles * 8 * kRlStatusStride, 16);  // ticket, error, status
         bytes = zero;
     }
@@ -2284,17 +1798,9 @@ extern "C" int flrl_rl_encode_device(const uint8_t *d_in, size_t n, uint8_t *d_c
     Ctrl *ctrl = static_cast<Ctrl *>(d_scratch);
     uint64_t *status = reinterpret_cast<uint64_t *>(static_cast<uint8_t *>(d_scratch) + kRlStatusOff);
     kernel_timing_begin(s);
-    if (FLRL_RL_LAG) {
-        const size_t slots = (size_t)FLRL_RL_LAG_PER_CU * (size_t)cu_count();
-        hipLaunchKernelGGL((rl_encode_lag_kernel<kRlLagWaves, kRlLaneBytes, kRlSub, FLRL_RL_LAG_STAGE>),
-                           dim3((uint32_t)(L.tiles < slots ? L.tiles : slots)), dim3(kRlLagThreads), 0, s, d_in,
-                           (uint64_t)n, (uint32_t)L.tiles, d_counts, d_values, d_runs, ctrl, status,
-                           lookback_help_ticks(kRlHelpTicks));
-    } else {
-        hipLaunchKernelGGL((rl_encode_wave_kernel<kRlThreads, kRlLaneBytes, kRlSub>), dim3((uint32_t)L.tiles),
-                           dim3(kRlThreads), 0, s, d_in, (uint64_t)n, (uint32_t)L.tiles, d_counts, d_values,
-                           d_runs, ctrl, status, lookback_help_ticks(kRlHelpTicks));
-    }
+    hipLaunchKernelGGL((rl_encode_wave_kernel<kRlThreads, kRlLaneBytes, kRlSub>), dim3((uint32_t)L.tiles),
+                       dim3(kRlThreads), 0, s, d_in, (uint64_t)n, (uint32_t)L.tiles, d_counts, d_values, d_runs,
+                       ctrl, status, lookback_help_ticks(kRlHelpTicks));
     kernel_timing_end(s);
     FLRL_HIP(hipGetLastError());
     return FLRL_OK;

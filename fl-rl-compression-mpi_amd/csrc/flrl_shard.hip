@@ -459,7 +459,8 @@ int encode_rank_impl(flrl_comm *c, const uint8_t *d_in, size_t n, uint8_t *d_bit
         if (local == FLRL_OK)
             local = set_error(FLRL_E_HIP, "flrl_fl_encode_rank: event wait failed");
         s = d.cstream;
-        // ordered on the host instead; failing that, send without touching the array
+        // ordered on the host instead; failing that, the slot is not written
+        // (the all-gather below still receives into the array: see there)
         staged = hipEventSynchronize(d.cdone) == hipSuccess;
     }
     uint64_t *slot = d.gather + shard_slot((uint64_t)c->rank, (uint64_t)c->nranks, 1);
@@ -476,9 +477,25 @@ int encode_rank_impl(flrl_comm *c, const uint8_t *d_in, size_t n, uint8_t *d_bit
         hipLaunchKernelGGL(put_pair_kernel, dim3(1), dim3(kWave), 0, s, slot, shard_failed_word(), (uint64_t)0);
         staged = hipGetLastError() == hipSuccess;
     }
-    const ncclResult_t r = staged ? ncclAllGather(slot, d.gather, 2, ncclUint64, d.nccl, s)  // in place
-                                  : ncclAllGather(d.red + 4, d.gather, 2, ncclUint64, d.nccl, d.cstream);
-    if (r != ncclSuccess || !staged) {
+    if (!staged) {
+        // The constant failed pair is sent from d.cstream, and the all-gather
+        // still RECEIVES into d.gather: order it after the previous call's scan
+        // (which may still read the array on the caller's stream) -- on the
+        // device, else on the host; if neither works the device is gone and
+        // the send goes ahead regardless, so that the peers are not left
+        // waiting in the collective.
+        if (hipStreamWaitEvent(d.cstream, d.cdone, 0) != hipSuccess)
+            (void)hipEventSynchronize(d.cdone);
+        const ncclResult_t r = ncclAllGather(d.red + 4, d.gather, 2, ncclUint64, d.nccl, d.cstream);
+        // the next call's slot write (ordered after d.cdone) must follow this
+        // all-gather's write of the array
+        if (r != ncclSuccess || hipEventRecord(d.cdone, d.cstream) != hipSuccess)
+            (void)hipStreamSynchronize(d.cstream);
+        (void)hipSetDevice(prev);
+        return local ? local : rccl_error(r, "ncclAllGather");
+    }
+    const ncclResult_t r = ncclAllGather(slot, d.gather, 2, ncclUint64, d.nccl, s);  // in place
+    if (r != ncclSuccess) {
         (void)hipSetDevice(prev);
         return local ? local : rccl_error(r, "ncclAllGather");
     }

@@ -324,12 +324,33 @@ struct MemFl {  // FL arrays in host memory
 // APIs take workers and chunk sizes at run time, so the cap also grows to
 // twice the most pinned memory ever leased at once (both directions of the
 // largest call shape seen): more or larger pipelines than the host API's do
-// not re-allocate on every call either.
+// not re-allocate on every call either. That growth is bounded
+// (ADVICE r05): it follows the most leased at once in the current and the last
+// kPoolEpochs busy periods (a busy period ends when no set is leased), so one
+// large call's pinned memory leaves the idle pool after a few smaller calls,
+// and it never exceeds an eighth of the host's physical memory.
 constexpr size_t kHostSetBound = 2 * (2 * (size_t)FLRL_HOST_CHUNK + (size_t)FLRL_HOST_CHUNK / 128 + 16);
 constexpr size_t kPoolBytes = 2 * (size_t)FLRL_HOST_WORKERS * kHostSetBound + (64ull << 20);
-size_t g_leased_bytes = 0;       // pinned bytes of the sets leased right now
-size_t g_peak_leased_bytes = 0;  // the most ever leased at once
-size_t pool_cap() { return std::max(kPoolBytes, 2 * g_peak_leased_bytes + ((size_t)64 << 20)); }
+constexpr int kPoolEpochs = 4;
+size_t g_leased_bytes = 0;                 // pinned bytes of the sets leased right now
+size_t g_epoch_peak = 0;                   // the most leased at once in the current busy period
+size_t g_epoch_peaks[kPoolEpochs] = {0};   // ... in the last kPoolEpochs busy periods
+int g_epoch_i = 0;
+size_t pool_ceiling()
+{
+    static const size_t c = [] {
+        const long pages = sysconf(_SC_PHYS_PAGES), psz = sysconf(_SC_PAGESIZE);
+        return pages > 0 && psz > 0 ? (size_t)pages * (size_t)psz / 8 : kPoolBytes;
+    }();
+    return std::max(kPoolBytes, c);
+}
+size_t pool_cap()
+{
+    size_t peak = g_epoch_peak;
+    for (size_t p : g_epoch_peaks)
+        peak = std::max(peak, p);
+    return std::min(pool_ceiling(), std::max(kPoolBytes, 2 * peak + ((size_t)64 << 20)));
+}
 struct PoolKey {
     int dev;
     size_t a, b, c, scr;
@@ -367,7 +388,7 @@ Slots *slots_acquire(int dev, size_t a, size_t b, size_t c, size_t scr)
     {
         std::lock_guard<std::mutex> g(g_pool_m);
         g_leased_bytes += k.pinned();  // (given back by slots_release, also for a failed lease)
-        g_peak_leased_bytes = std::max(g_peak_leased_bytes, g_leased_bytes);
+        g_epoch_peak = std::max(g_epoch_peak, g_leased_bytes);
         for (auto it = g_pool.rbegin(); it != g_pool.rend(); ++it)
             if (it->key == k) {
                 Slots *x = it->x;
@@ -398,6 +419,11 @@ void slots_release(Slots *x, size_t a, size_t b, size_t c, size_t scr)
     {
         std::lock_guard<std::mutex> g(g_pool_m);
         g_leased_bytes -= PoolKey{0, a, b, c, scr}.pinned();
+        if (g_leased_bytes == 0) {  // a busy period ends
+            g_epoch_peaks[g_epoch_i] = g_epoch_peak;
+            g_epoch_i = (g_epoch_i + 1) % kPoolEpochs;
+            g_epoch_peak = 0;
+        }
     }
     if (!x)
         return;

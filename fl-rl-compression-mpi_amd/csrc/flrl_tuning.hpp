@@ -17,8 +17,7 @@
      defined(FLRL_RL_STAGE) || defined(FLRL_RL_WPS) || defined(FLRL_RD_NARROW_MEAN) || defined(FLRL_RL_RO_MAXB) ||          \
      defined(FLRL_RD_UNROLL) || defined(FLRL_HOST_WORKERS) || defined(FLRL_HOST_CHUNK) ||                \
      defined(FLRL_HOST_DIRECT) || defined(FLRL_HOST_PROFILE) || defined(FLRL_HOST_THP) || defined(FLRL_RL_WD64_MEAN) || defined(FLRL_RL_DENSE_MEAN) ||\
-     defined(FLRL_RL_LAG) || defined(FLRL_RL_LAG_WPS) || defined(FLRL_RL_LAG_PER_CU) || defined(FLRL_RL_LAG_STAGE) || defined(FLRL_RL_LAG_GUARD) || defined(FLRL_RL_LAG_WAVES) || defined(FLRL_RL_LAG_EMIT) || defined(FLRL_RL_LAG_PF) ||\
-     defined(FLRL_FL_STORE_SPLIT) || defined(FLRL_FL_STORE_SKIP) || defined(FLRL_RL_SUB) || defined(FLRL_RL_FLUSH_NT) || defined(FLRL_RD_WAVE_NT) || defined(FLRL_ABL_FLUSH) || defined(FLRL_RL_DENSE_PF_EARLY) || defined(FLRL_ABL_RD) || defined(FLRL_RD_BPERM))
+     defined(FLRL_FL_STORE_SPLIT) || defined(FLRL_FL_STORE_SKIP) || defined(FLRL_RL_SUB))
 #error "FLRL_* kernel overrides are for timing harnesses only (define FLRL_TUNING_BUILD)"
 #endif
 
@@ -45,24 +44,6 @@
 #endif
 #ifndef FLRL_RL_SUB
 #define FLRL_RL_SUB 8  // RL encode: 4 KiB sub-chunks per wave chunk (8: 32 KiB chunks, 128 KiB tiles)
-#endif
-#ifndef FLRL_RL_FLUSH_NT
-#define FLRL_RL_FLUSH_NT 0  // RL encode: non-temporal 16-byte stores for dense (piece-staged) records
-#endif
-#ifndef FLRL_RD_WAVE_NT
-#define FLRL_RD_WAVE_NT 0  // RL wave decode (dense inputs): non-temporal 16-byte output stores
-#endif
-#ifndef FLRL_ABL_FLUSH
-#define FLRL_ABL_FLUSH 0  // timing-only ablations of the dense RL flush (1: no gather, 2: no stores)
-#endif
-#ifndef FLRL_RL_DENSE_PF_EARLY
-#define FLRL_RL_DENSE_PF_EARLY 0  // RL encode re-read: next sub-chunk's load issued before the dense pieces
-#endif
-#ifndef FLRL_ABL_RD
-#define FLRL_ABL_RD 0  // timing-only ablations of the RL block decode (1: no assembly, 2: no marks, 4: no stores, 8: whole-chunk stores only)
-#endif
-#ifndef FLRL_RD_BPERM
-#define FLRL_RD_BPERM 0  // RL block decode: sparse windows' chunk values by ds_bpermute from registers
 #endif
 #ifndef FLRL_FL_LOOKG
 #define FLRL_FL_LOOKG 1  // FL encode look-back granules per lane (window 64 G tiles)
@@ -110,39 +91,6 @@
 // 4-wave workgroups per CU, at most 96 VGPRs).
 #ifndef FLRL_RL_WPS
 #define FLRL_RL_WPS 5
-#endif
-
-// RL encode form: 1 = persistent workgroups with a look-back wave one tile
-// behind the scan (rl_encode_lag_kernel), 0 = one tile per workgroup
-// (rl_encode_wave_kernel).
-#ifndef FLRL_RL_LAG
-#define FLRL_RL_LAG 0
-#endif
-// persistent form: data waves per workgroup (+ the look-back wave: 4 waves,
-// one per SIMD -- a 5-wave workgroup of 4 data waves placed unevenly, and only
-// two per CU were ever resident), workgroups per CU, the waves per SIMD they
-// are compiled for, and each of the two staging buffers (bytes per workgroup;
-// five per CU leave 2 x 9600 beside the 12 KiB images)
-#ifndef FLRL_RL_LAG_WAVES
-#define FLRL_RL_LAG_WAVES 3
-#endif
-#ifndef FLRL_RL_LAG_PER_CU
-#define FLRL_RL_LAG_PER_CU 5
-#endif
-#ifndef FLRL_RL_LAG_WPS
-#define FLRL_RL_LAG_WPS 5
-#endif
-#ifndef FLRL_RL_LAG_STAGE
-#define FLRL_RL_LAG_STAGE 9600
-#endif
-// persistent form: staged runs emitted by the data waves at the top of their
-// next tile (1) or by the look-back wave (0)
-#ifndef FLRL_RL_LAG_EMIT
-#define FLRL_RL_LAG_EMIT 1
-#endif
-// persistent form: sub-chunks in flight per data wave
-#ifndef FLRL_RL_LAG_PF
-#define FLRL_RL_LAG_PF FLRL_RL_PF
 #endif
 
 // ---- RL decode shape ---------------------------------------------------------

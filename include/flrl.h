@@ -169,7 +169,15 @@ int flrl_fl_encode_rank(flrl_comm *c, const uint8_t *d_in, size_t n, uint8_t *d_
  * Collective on errors too: a rank that fails (allocation, upload, device
  * error, rank 0's merge buffer) still completes the exchange and an all-reduce
  * of {size, failed}, so every rank returns an error and none waits in the
- * payload send/recv. */
+ * payload send/recv.
+ * ONE EXCEPTION (not collective): a device that fails between that all-reduce
+ * and copying its result to the host (csrc/flrl_shard.hip, the read-back after
+ * ncclAllReduce). That rank cannot learn whether the payload step runs, so it
+ * returns FLRL_E_HIP without joining it; if no rank had failed before, its
+ * peers then block in the payload ncclSend/ncclRecv as in any collective with
+ * a dead member (RCCL's own behaviour; the job's launcher has to end the
+ * ranks). A second confirmation round would only move this window, not close
+ * it. */
 int flrl_fl_compress_rank(flrl_comm *c, const uint8_t *data, size_t size, flrl_fl_buf *out);
 
 /* The exchange's layout, host-callable (the device scan runs the same code,
@@ -295,7 +303,8 @@ int flrl_debug_fail_chunk(long long chunk);
 
 /* Test hook: the next flrl_fl_encode_rank / flrl_fl_compress_rank call of this
  * thread fails once at `step`, as the runtime call there would, to exercise the
- * collective-on-error paths (every rank still completes every collective):
+ * collective-on-error paths (every rank still completes every collective,
+ * except after FLRL_DEBUG_RANK_READ_SUM):
  *   FLRL_DEBUG_RANK_SET_DEVICE   the rank cannot reach its device: its exchange
  *                                slot is sent from the comm's constant failed pair
  *   FLRL_DEBUG_RANK_STREAM_WAIT  the stream cannot be ordered after the previous
@@ -303,7 +312,10 @@ int flrl_debug_fail_chunk(long long chunk);
  *   FLRL_DEBUG_RANK_STAGE_WORD   (compress_rank) the {size, failed} word cannot be
  *                                staged: the constant {0, 1} is reduced instead
  *   FLRL_DEBUG_RANK_READ_SUM     (compress_rank) the reduced word cannot be read
- *                                back (a device failure after the all-reduce)
+ *                                back (a device failure after the all-reduce; the
+ *                                one case that is NOT collective: with two or more
+ *                                ranks and no earlier failure the peers then wait
+ *                                in the payload send/recv, see flrl_fl_compress_rank)
  * 0 cancels. Never needed by callers. */
 #define FLRL_DEBUG_RANK_SET_DEVICE 1
 #define FLRL_DEBUG_RANK_STREAM_WAIT 2

@@ -20,7 +20,7 @@ import statistics
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 KMAP = {"fl_encode_kernel": "fl_encode", "fl_decode_kernel": "fl_decode",
-        "fl_offsets_kernel": "fl_offsets", "rl_encode_wave_kernel": "rl_encode", "rl_encode_lag_kernel": "rl_encode", "rl_encode_kernel": "rl_encode",
+        "fl_offsets_kernel": "fl_offsets", "rl_encode_wave_kernel": "rl_encode",
         "rl_encode_scan_kernel": "rl_encode_scan", "rl_encode_state_kernel": "rl_encode_state",
         "rl_encode_emit_kernel": "rl_encode_emit",
         "rl_decode_kernel": "rl_decode", "rl_decode_wave_kernel": "rl_decode_wave", "rl_offsets_kernel": "rl_offsets",

@@ -60,3 +60,21 @@ def test_rank_shard_weak_and_strong():
         raise AssertionError("a rank without a frame must be refused")
     except SystemExit:
         pass
+
+
+def test_cpu_baseline_on_every_line():
+    """VERDICT r05 missing item 2: north_star asks for the fl-cpu / rl-cpu
+    figure "in the same run" at 1, 2, 4 and 8 GPUs, so rank 0 of an N > 1 line
+    carries `cpu_baseline` too (FL on the first bytes of its shard, plus the RL
+    oracle, which at N = 1 the RL section times itself); other ranks carry none,
+    and --cpu-sample 0 skips it."""
+    n = 1 << 20
+    for world in (1, 2, 8):
+        cpu = bench.line_cpu_baseline(0, world, "u8", 42, n)
+        assert cpu is not None and cpu["value"] > 0 and cpu["cores"] == 1 and cpu["kind"] == "port"
+        assert cpu["roundtrip_ok"]
+        assert ("rl" in cpu) == (world > 1)
+        if world > 1:
+            assert cpu["rl"]["value"] > 0 and cpu["rl"]["roundtrip_ok"] and cpu["rl"]["runs"] > n // 64
+        assert bench.line_cpu_baseline(1, world, "u8", 42, n) is None
+    assert bench.line_cpu_baseline(0, 2, "u8", 42, 0) is None

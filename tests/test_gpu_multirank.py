@@ -4,7 +4,12 @@ run by two processes over an RCCL communicator. One case checks the merged
 result on rank 0 against the single-GPU encode of the whole input; the others
 inject a failure on rank 1 at each collective step (flrl_debug_fail_rank_step)
 and check that BOTH ranks return an error within a time limit instead of
-waiting in a collective. Needs two visible GPUs; skipped otherwise (the round's
+waiting in a collective. FLRL_DEBUG_RANK_READ_SUM is deliberately not among
+them: a device that fails after the {size, failed} all-reduce but before its
+result reaches the host is the one documented non-collective case
+(include/flrl.h, flrl_fl_compress_rank) -- its peers wait in the payload
+send/recv, so that case would hang here by design. Needs two visible GPUs;
+skipped otherwise (the round's
 one-GPU box runs the same steps on a one-rank communicator in
 tests/test_gpu_shard.py)."""
 import os

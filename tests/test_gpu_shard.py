@@ -314,6 +314,37 @@ def test_encode_rank_runtime_failure_still_exchanges(rank_comm, step):
     assert torch.equal(d.decode(rec[flrl.SZ_V]), x)
 
 
+@pytest.mark.parametrize("step", [flrl.DEBUG_RANK_SET_DEVICE, flrl.DEBUG_RANK_STREAM_WAIT])
+def test_encode_rank_failure_between_calls_without_sync(rank_comm, step):
+    """a failed call whose slot could not be staged sends
+    the comm's constant failed pair from the comm's stream, and that all-gather
+    still RECEIVES into the gather array. Issued right behind a good call and
+    right before another, with no host synchronisation in between, it must not
+    overwrite the array while the earlier call's size scan is still pending on
+    the caller's stream, nor after the next call's slot write: both good calls
+    keep their records and their scratch error words stay 0. 256 MiB inputs
+    keep the earlier call's scan queued behind its encode when the failed call
+    is issued."""
+    from flrl.device import FLDevice
+    n = 256 << 20
+    x = torch.randint(0, 256, (n,), dtype=torch.uint8, device="cuda")
+    a, f, b = FLDevice(n), FLDevice(n), FLDevice(n)
+    torch.cuda.synchronize()
+    for _ in range(3):
+        a.encode_rank(rank_comm, x)
+        flrl.debug_fail_rank_step(step)
+        with pytest.raises(flrl.FLRLError) as e:
+            f.encode_rank(rank_comm, x)
+        assert e.value.code == flrl.E_HIP
+        b.encode_rank(rank_comm, x)
+        torch.cuda.synchronize()
+        for name, d in (("first", a), ("next", b)):
+            rec = [int(t) for t in d.rank_sizes[:flrl.SZ_COUNT].cpu()]
+            assert rec == [n // 128, n, 0, 0, n // 128, n], (name, rec)
+            assert d.error() == 0, name
+    flrl.debug_fail_rank_step(0)
+
+
 @pytest.mark.parametrize("step", [flrl.DEBUG_RANK_SET_DEVICE, flrl.DEBUG_RANK_STREAM_WAIT,
                                   flrl.DEBUG_RANK_STAGE_WORD, flrl.DEBUG_RANK_READ_SUM])
 def test_compress_rank_runtime_failure_returns(rank_comm, golden, bmp_bytes, step):

@@ -433,6 +433,31 @@ def test_alternating_file_calls_keep_larger_staging(tmp_path):
     assert freed >= 2 * W * 2 * (2 * C), freed
 
 
+def test_large_file_staging_leaves_the_pool_after_smaller_calls(tmp_path):
+    """the idle-pool cap used to grow to twice the largest lease
+    ever seen and never shrink, so one call with many pipelines or large
+    chunks kept that much pinned host memory idle for the rest of the process.
+    The cap now follows the last few busy periods only: after a large file call
+    and a handful of host-API calls the idle pool is back within the host API's
+    own bound (8 pipelines x 2 directions of 16 MiB-chunk sets + 64 MiB)."""
+    import flrl
+    W, C = 12, 32 << 20
+    a = oracle.gen("lo4", W * C + 5, 29)
+    src, enc, back = tmp_path / "in", tmp_path / "enc", tmp_path / "back"
+    src.write_bytes(a.tobytes())
+    flrl.release_staging()
+    flrl.fl_compress_file(str(src), str(enc), W, C)
+    flrl.fl_decompress_file(str(enc), str(back), W, C)
+    assert back.read_bytes() == a.tobytes()
+    small = oracle.gen("lo4", (128 << 20) + 3, 21)
+    for _ in range(3):
+        c = flrl.fl_compress(small)
+        assert np.array_equal(flrl.fl_decompress(small.size, c.bits, c.values), small)
+    freed = flrl.release_staging()
+    host_bound = 2 * 8 * 2 * (2 * (16 << 20) + (16 << 20) // 128 + 16) + (64 << 20)
+    assert 2 * 8 * 2 * (32 << 20) <= freed <= host_bound, freed
+
+
 def test_release_staging_frees_idle_sets():
     """The host API keeps its pinned staging between calls (bounded); releasing
     it frees the idle sets, and the next call allocates afresh."""
