@@ -247,10 +247,14 @@ __global__ __launch_bounds__(T + kWave, 1) void fl_encode_kernel(
             // ---- the look-back wave: publish, resolve (concurrent with the pack;
             // it issues no bulk loads or stores, so its status loads never wait
             // behind them -- vmcnt is per wave and in order)
+#if FLRL_FL_STATIC_W  // PMC/timing builds only: every frame at width W, no status traffic
+            const uint64_t excl = (uint64_t)tile * TF * FLRL_FL_STATIC_W;
+#else
             if (tid == T)
                 publish_aggregate<FLRL_FL_STATUS_STRIDE>(status, tile, agg);
             FLRL_FL_TRACE(tile, 1);
             const uint64_t excl = lookback_resolve<FLRL_FL_LOOKG, FLRL_FL_LOOKL, FLRL_FL_STATUS_STRIDE>(status, tile, agg, ctrl);
+#endif
             if (tid == T)
                 s_base = excl;
             FLRL_FL_TRACE(tile, 2);

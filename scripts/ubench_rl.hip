@@ -48,10 +48,22 @@ __device__ __forceinline__ uint64_t rl_rtime()
     asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
     return t;
 }
+// slot 7 (at k == 0): where the tile ran -- XCC id << 32 | HW_ID (wave, SIMD,
+// CU, SH, SE fields)
+__device__ __forceinline__ uint64_t rl_where()
+{
+    uint32_t hw, xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    return ((uint64_t)xcc << 32) | hw;
+}
 #define FLRL_RL_TRACE(tile, k)                                                   \
     do {                                                                         \
-        if ((threadIdx.x & 63) == 0)                                             \
-            g_trace[(uint64_t)(tile) * 8 + (k)] = rl_rtime(); \
+        if ((threadIdx.x & 63) == 0) {                                           \
+            g_trace[(uint64_t)(tile) * 8 + (k)] = rl_rtime();                    \
+            if ((k) == 0)                                                        \
+                g_trace[(uint64_t)(tile) * 8 + 7] = rl_where();                  \
+        }                                                                        \
     } while (0)
 #define FLRL_RL_LB_STAT(tile, spins, rounds)                                      \
     do {                                                                          \
@@ -105,10 +117,17 @@ int main(int argc, char **argv)
             return 1;
         }
         CK(hipMemcpy(d_in, h, n, hipMemcpyHostToDevice));
+        if (getenv("INPUT_OUT")) {  // the input, for per-tile statistics on the host
+            FILE *f = fopen(getenv("INPUT_OUT"), "wb");
+            if (f) {
+                fwrite(h, 1, n, f);
+                fclose(f);
+            }
+        }
         free(h);
     }
 #ifdef TRACE
-    const size_t ntiles = (n + flrl::kRlEncTileBytes - 1) / flrl::kRlEncTileBytes;  // tiles of the shipped form
+    const size_t ntiles = (n + flrl::kRlTileBytes - 1) / flrl::kRlTileBytes;
     uint64_t *d_tr;
     CK(hipMalloc(&d_tr, ntiles * 64));
     CK(hipMemset(d_tr, 0, ntiles * 64));
