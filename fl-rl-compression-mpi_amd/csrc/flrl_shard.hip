@@ -133,8 +133,9 @@ int dev_setup(Dev &d, size_t gather_entries)
         }
     }
     if (gather_entries > d.gather_cap) {
-        if (d.gather) {  // the previous call's exchange may still read it
+        if (d.gather) {  // the previous call's exchange or scan may still read it
             (void)hipStreamSynchronize(d.cstream);
+            (void)hipEventSynchronize(d.cdone);  // (a per-rank call's scan ran on the caller's stream)
             (void)hipFree(d.gather);
             d.gather = nullptr;
             d.gather_cap = 0;
@@ -156,6 +157,8 @@ void dev_release(Dev &d, bool destroy_nccl)
     (void)hipSetDevice(d.id);
     if (d.cstream)
         (void)hipStreamSynchronize(d.cstream);
+    if (d.cdone)  // the last per-rank call's size scan (on the caller's stream) reads the gather array
+        (void)hipEventSynchronize(d.cdone);
     if (d.gather)
         (void)hipFree(d.gather);
     if (d.red)

@@ -345,6 +345,27 @@ def test_encode_rank_failure_between_calls_without_sync(rank_comm, step):
     flrl.debug_fail_rank_step(0)
 
 
+def test_comm_destroy_right_after_encode_rank():
+    """A per-rank call's size scan runs on the caller's stream and reads the
+    comm's gather array; destroying the comm right after the call (no host
+    synchronisation) waits for that scan before freeing the array, so the
+    record is still the right one."""
+    from flrl.device import FLDevice
+    torch.cuda.set_device(0)
+    n = 256 << 20
+    x = torch.randint(0, 256, (n,), dtype=torch.uint8, device="cuda")
+    d = FLDevice(n)
+    torch.cuda.synchronize()
+    for _ in range(2):
+        c = flrl.Comm.rank(1, flrl.comm_unique_id(), 0)
+        d.rank_sizes = torch.full((8,), -1, dtype=torch.int64, device="cuda")
+        d.encode_rank(c, x)
+        c.destroy()
+        torch.cuda.synchronize()
+        assert [int(t) for t in d.rank_sizes[:flrl.SZ_COUNT].cpu()] == [n // 128, n, 0, 0, n // 128, n]
+        assert d.error() == 0
+
+
 @pytest.mark.parametrize("step", [flrl.DEBUG_RANK_SET_DEVICE, flrl.DEBUG_RANK_STREAM_WAIT,
                                   flrl.DEBUG_RANK_STAGE_WORD, flrl.DEBUG_RANK_READ_SUM])
 def test_compress_rank_runtime_failure_returns(rank_comm, golden, bmp_bytes, step):
