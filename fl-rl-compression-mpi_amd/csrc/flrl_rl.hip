@@ -1072,7 +1072,12 @@ __global__ __launch_bounds__(T, kRlWavesPerSimd) void rl_encode_wave_kernel(  //
         FLRL_RL_TRACE(tile, 2);
         // decoupled fallback: a predecessor tile's map from its input
         auto help = [&](uint32_t t) -> uint64_t { return rl_tile_map_slow<Wv::TBT>(in, n, t); };
+#if FLRL_RL_PMC_NOLB  // PMC builds only (output wrong): no status traffic, every tile at state (0, 0)
+        uint64_t st = sm_const(0, 0);
+        (void)help;
+#else
         uint64_t st = lookback_seg<kRlLookG, kRlLookL, kRlStatusStride>(status, tile, tmap, ctrl, help_ticks, help);
+#endif
         FLRL_RL_TRACE(tile, 3);
         if (V.lane == 0) {
 #pragma unroll
