@@ -102,3 +102,31 @@ def test_rl_structured_vs_oracle(seed):
     assert np.array_equal(d.values[:r].cpu().numpy(), values)
     assert torch.equal(d.decode(r), x)
     assert d.error() == 0
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_file_paths_structured_vs_oracle(tmp_path, seed):
+    """The streamed file paths (chunked pipelines; RL runs re-split across chunk
+    boundaries by the in-order writer) on the same structured inputs, with a
+    random chunk size and worker count per seed: the .fl file equals the
+    oracle's bytes (the reference fl-cpu format), the RL file the oracle's
+    records in the build's container, and both decompress back."""
+    import flrl
+    rng = np.random.default_rng(3000 + seed)
+    a = structured(3000 + seed)
+    src = tmp_path / "in"
+    a.tofile(src)
+    workers = int(rng.integers(1, 5))
+    fl_chunk = int(rng.choice([0, 128 * int(rng.integers(1, 64)), 128 * int(rng.integers(64, 8192))]))
+    rl_chunk = int(rng.choice([0, int(rng.integers(256, 5000)), int(rng.integers(5000, 1 << 20))]))
+    enc, back = tmp_path / "out.fl", tmp_path / "back"
+    flrl.fl_compress_file(str(src), str(enc), workers, fl_chunk)
+    assert enc.read_bytes() == oracle.fl_file_bytes(a), (workers, fl_chunk)
+    flrl.fl_decompress_file(str(enc), str(back), workers, fl_chunk)
+    assert back.read_bytes() == a.tobytes()
+    enc = tmp_path / "out.rl"
+    flrl.rl_compress_file(str(src), str(enc), workers, rl_chunk)
+    counts, values = oracle.rl_compress(a)
+    assert enc.read_bytes() == flrl.rl_file_bytes(a.size, counts, values), (workers, rl_chunk)
+    flrl.rl_decompress_file(str(enc), str(back), workers, rl_chunk)
+    assert back.read_bytes() == a.tobytes()
