@@ -443,6 +443,7 @@ struct RlWave {
     static constexpr int kLdsBytes = W * WB + STG;
     static_assert(LB == 64, "one u64 head mask per lane (piece emission: 4 x 16 positions)");
     static_assert(TBT == kRlTileBytes, "tile geometry shared with the layout");
+    static_assert(SW >= 16 * LB + 15, "a piece part (16 rows) and the carried records fit the staging");
 
     struct Sub {
         uint32_t nat[CH / 2];  // 16-bit natural-head masks, two per word
@@ -679,24 +680,33 @@ struct RlWave {
         const uint32_t up = wave_shr1(x.w >> 24);  // lane t-1 holds piece k-1 of the same row when k > 0
         const uint32_t pb = k == 0 ? pr : up;      // the byte before the piece
         const uint64_t below = k == 0 ? 0ull : m & ((1ull << (16 * k)) - 1);
-        uint32_t rank = sr + (uint32_t)__popcll(below) - base;
+        const uint32_t rank0 = sr + (uint32_t)__popcll(below) - base;
         // count of a head at pos = pos - prev; before the row's first head prev
-        // is -c (the state before the row): c + pos <= 255 by the 255-split rule
-        int32_t prev = below ? 63 - __builtin_clzll(below) : -(int32_t)cr;
+        // is -c (the state before the row): c + pos <= 255 by the 255-split
+        // rule, and the state 0 (255 bytes) has its head at pos 0, so every
+        // count is in [1, 255]
+        // (prev relative to the piece: the positions are then immediates, not
+        // sixteen registers of 16k + i)
+        int32_t prev = (below ? 63 - __builtin_clzll(below) : (cr == 0 ? -255 : -(int32_t)cr)) - 16 * k;
         const uint32_t m16 = (uint32_t)(m >> (16 * k)) & 0xFFFFu;
+        uint32_t rank = rank0;
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
-            const bool h = (m16 >> i) & 1u;
-            const int32_t pos = 16 * k + i;
-            const uint32_t cnt = (uint32_t)(pos - prev);
+            // heads at positions <= i (bits 0..i moved to the top): position
+            // i is a head iff it raises the rank
+            // (v_bcnt with the add folded in: written as a sum, the compiler
+            // compares the two popcounts and adds rank0 again under the head)
+            uint32_t rnext;
+            asm("v_bcnt_u32_b32 %0, %1, %2" : "=v"(rnext) : "v"(m16 << (31 - i)), "v"(rank0));
+            const int32_t pos = i;
             const uint32_t val = i == 0 ? pb : (x[(i - 1) >> 2] >> (8 * ((i - 1) & 3))) & 0xFFu;
-            const uint32_t at = pswz(rank);
-            if (h) {
-                stc[at] = (uint8_t)(cnt == 0 ? 255u : cnt);
+            if (rnext != rank) {
+                const uint32_t at = pswz(rank);
+                stc[at] = (uint8_t)(pos - prev);
                 stv[at] = (uint8_t)val;
+                prev = pos;
             }
-            rank += h ? 1u : 0u;
-            prev = h ? pos : prev;
+            rank = rnext;
         }
     }
 
@@ -717,20 +727,29 @@ struct RlWave {
     // Records [0, nrec) of a piece-staged part to counts/values at global record
     // index g0 + j, i.e. byte g0 + j - 1 (the input's first head, g0 + j == 0,
     // ends no run): one 16-byte store per lane and array for every aligned
-    // chunk inside the range, 1/2/4/8-byte pieces for the two it shares.
-    __device__ void piece_flush(uint32_t nrec, uint64_t g0, uint8_t *__restrict__ counts,
-                                uint8_t *__restrict__ values) const
+    // chunk inside the range, 1/2/4/8-byte pieces for a chunk the range shares.
+    // Unless `last`, the records of a trailing partial chunk are not stored but
+    // moved to staging [0, keep) (returned) and go out with the next part: a
+    // dense run of parts then stores whole chunks only, one instruction per
+    // lane and array (a part is <= 1024 records + the carry, <= 64 chunks
+    // after the first), apart from its first and last chunk.
+    __device__ uint32_t piece_flush(uint32_t nrec, uint64_t g0, bool last, uint8_t *__restrict__ counts,
+                                    uint8_t *__restrict__ values) const
     {
         const uint32_t j0 = g0 == 0 ? 1u : 0u;
         if (nrec <= j0)
-            return;
+            return last ? 0u : nrec;
         // destination bytes [A, E) = [g0 + j0 - 1, g0 + nrec - 1), in 16-byte
         // chunks from the one holding A; chunk q starts at record (q - h) * 16 - a
         const uint64_t A = g0 + j0 - 1;
         const uint32_t a = (uint32_t)(A & 15u);  // A's offset in its chunk
         const uint32_t span = a + (nrec - j0);   // bytes from the chunk start to E
+        // kept: the records of the chunk holding E - 1 when it is partial (all
+        // of them when that chunk is also A's)
+        const uint32_t keep = last || (span & 15u) == 0 ? 0u : (span < 16 ? nrec : (span & 15u));
+        const uint32_t stop = span - ((span & 15u) && !last ? (span & 15u) : 0u);
         uint8_t *const pc = counts + (A - a), *const pv = values + (A - a);
-        for (uint32_t q = (uint32_t)lane; 16 * q < span; q += kWave) {
+        for (uint32_t q = (uint32_t)lane; 16 * q < stop; q += kWave) {
             const int32_t o = (int32_t)(16 * q) - (int32_t)a + (int32_t)j0;  // record of the chunk's first byte
             const uint32_t lo = q == 0 ? a : 0u;
             const uint32_t hi = span - 16 * q < 16 ? span - 16 * q : 16u;
@@ -745,6 +764,21 @@ struct RlWave {
                 }
             }
         }
+        if (keep != 0 && keep != nrec) {  // wave-uniform; the wave's reads all precede its writes
+            const uint32_t j = (uint32_t)lane;
+            uint32_t c = 0, v = 0;
+            if (j < keep) {
+                const uint32_t from = pswz(nrec - keep + j);
+                c = stc[from];
+                v = stv[from];
+            }
+            if (j < keep) {
+                const uint32_t to = pswz(j);
+                stc[to] = (uint8_t)c;
+                stv[to] = (uint8_t)v;
+            }
+        }
+        return keep;
     }
 
     // The staging pass over the chunk at `off` (`len` bytes): every sub-chunk's
@@ -846,6 +880,9 @@ struct RlWave {
         uint32_t pb = uniform32(re_off > 0 ? (uint32_t)in[re_off - 1] : 0u);
         u32x4 pf[NJ];
         load_sub(off, s0, pf);
+        // records of the piece parts not yet stored (a partial last chunk),
+        // staged at [0, carry): global record indices hb - carry .. hb - 1
+        uint32_t carry = 0;
         for (int s = s0; s < ns; ++s) {
             // the previous sub-chunk's reads of the staging and the image are
             // this wave's own LDS ops: in order
@@ -865,6 +902,11 @@ struct RlWave {
                 // stage at (g - hb), store contiguously
                 if (s + 1 < ns)
                     load_sub(off, s + 1, pf);
+                if (carry) {  // the pieces' last records first: the staging is reused
+                    piece_flush(carry, hb - carry, true, counts, values);
+                    carry = 0;
+                    wave_lds_sync();
+                }
                 lane_runs(L, hm0, hm1, c_lane, (uint32_t)(g - hb));
                 wave_lds_sync();
                 for (uint32_t j = lane; j < hs; j += kWave) {
@@ -876,16 +918,17 @@ struct RlWave {
                 }
                 wave_lds_sync();
             } else {
-                // four parts of 16 rows (<= 1024 records each, within the staging),
-                // each staged by piece_part and stored with 16-byte stores
+                // four parts of 16 rows (<= 1024 records each + the carry, within
+                // the staging), each staged by piece_part after the carried records
+                // and stored with 16-byte stores
                 const uint32_t sl = (uint32_t)(g - hb);
 #pragma unroll 1
                 for (int p = 0; p < kWave / 16; ++p) {
                     const uint32_t b0 = (uint32_t)__builtin_amdgcn_readlane((int)sl, 16 * p);
                     const uint32_t b1 = p + 1 < kWave / 16 ? (uint32_t)__builtin_amdgcn_readlane((int)sl, 16 * (p + 1)) : hs;
-                    piece_part(p, hm0, c_lane, sl, L.p0, b0);
+                    piece_part(p, hm0, c_lane, sl, L.p0, b0 - carry);
                     wave_lds_sync();
-                    piece_flush(b1 - b0, hb + b0, counts, values);
+                    carry = uniform32(piece_flush(carry + (b1 - b0), hb + b0 - carry, false, counts, values));
                     wave_lds_sync();
                 }
             }
@@ -894,6 +937,8 @@ struct RlWave {
             hb += hs;
             rel = pm_compose(rel, L.smap);
         }
+        if (carry)
+            piece_flush(carry, hb - carry, true, counts, values);
     }
 
     // Emission of chunk C with the state (heads before it, chunk state) at its
