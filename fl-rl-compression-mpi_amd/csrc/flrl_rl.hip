@@ -444,6 +444,8 @@ struct RlWave {
     static_assert(LB == 64, "one u64 head mask per lane (piece emission: 4 x 16 positions)");
     static_assert(TBT == kRlTileBytes, "tile geometry shared with the layout");
     static_assert(SW >= 16 * LB + 15, "a piece part (16 rows) and the carried records fit the staging");
+    static constexpr uint32_t kPieceSink = 1152;  // piece_part's sink bytes (4 per lane) in stc/stv
+    static_assert(kPieceSink >= 16 * LB + 16 && kPieceSink + 4 * kWave <= SW, "sink past the part's records");
 
     struct Sub {
         uint32_t nat[CH / 2];  // 16-bit natural-head masks, two per word
@@ -658,8 +660,10 @@ struct RlWave {
     // .. 16k+15) of row 16p + t / 4, so every lane is busy whatever the density,
     // and walks its 16 positions unrolled: values from the piece's bytes in
     // registers, counts from the previous head's position (or the row's state
-    // before its first head). (Branch-free stores through a sink address for
-    // non-heads: runs32 +3 %, random bytes +12 %.) Record j of the part (j = record - base < 1024) goes to
+    // before its first head); non-heads store to a sink byte of their own lane
+    // (round 3's single sink address for all lanes was 12 % slower than a
+    // branch per position; one per lane is 1 % faster). Record j of the part
+    // (j = record - base + carry < 1024 + 15) goes to
     // stc/stv[pswz(j)]: the swizzle spreads the 64 lanes' stores, 16 rows x 4
     // pieces about 64 records apart, over all 64 banks. (Replaced one-row-at-
     // a-time emission, whose readlane/rank work per row made dense inputs 3.7x
@@ -700,12 +704,13 @@ struct RlWave {
             asm("v_bcnt_u32_b32 %0, %1, %2" : "=v"(rnext) : "v"(m16 << (31 - i)), "v"(rank0));
             const int32_t pos = i;
             const uint32_t val = i == 0 ? pb : (x[(i - 1) >> 2] >> (8 * ((i - 1) & 3))) & 0xFFu;
-            if (rnext != rank) {
-                const uint32_t at = pswz(rank);
-                stc[at] = (uint8_t)(pos - prev);
-                stv[at] = (uint8_t)val;
-                prev = pos;
-            }
+            // (non-heads to a per-lane sink byte past the part's records
+            // instead of a branch per position: random bytes -1 %)
+            const bool h = rnext != rank;
+            const uint32_t at = h ? pswz(rank) : kPieceSink + 4u * (uint32_t)lane;
+            stc[at] = (uint8_t)(pos - prev);
+            stv[at] = (uint8_t)val;
+            prev = h ? pos : prev;
             rank = rnext;
         }
     }
@@ -749,18 +754,38 @@ struct RlWave {
         const uint32_t keep = last || (span & 15u) == 0 ? 0u : (span < 16 ? nrec : (span & 15u));
         const uint32_t stop = span - ((span & 15u) && !last ? (span & 15u) : 0u);
         uint8_t *const pc = counts + (A - a), *const pv = values + (A - a);
-        for (uint32_t q = (uint32_t)lane; 16 * q < stop; q += kWave) {
-            const int32_t o = (int32_t)(16 * q) - (int32_t)a + (int32_t)j0;  // record of the chunk's first byte
-            const uint32_t lo = q == 0 ? a : 0u;
-            const uint32_t hi = span - 16 * q < 16 ? span - 16 * q : 16u;
+        if (a == 0 && j0 == 0) {
+            // chunk q = staged records 16q .. 16q+15, one aligned 16-byte group
+            // whose dwords pswz permutes by t = bits 8-9 of 16q: dword i at i ^ t
+            for (uint32_t q = (uint32_t)lane; 16 * q < stop; q += kWave) {
+                const uint32_t t = (q >> 4) & 3u;
+                const uint32_t hi = span - 16 * q < 16 ? span - 16 * q : 16u;
 #pragma unroll
-            for (int arr = 0; arr < 2; ++arr) {
-                const u32x4 v = piece_gather(arr ? stv : stc, o);
-                uint8_t *const d = (arr ? pv : pc) + 16 * q;
-                if (lo == 0 && hi == 16) {
-                    *reinterpret_cast<u32x4 *>(d) = v;  // (non-temporal: +-0.2 %)
-                } else {
-                    store_chunk_part(d, v, lo, hi);
+                for (int arr = 0; arr < 2; ++arr) {
+                    const u32x4 r = *reinterpret_cast<const u32x4 *>((arr ? stv : stc) + 16 * q);
+                    const u32x4 s = (t & 1u) ? u32x4{r.y, r.x, r.w, r.z} : r;
+                    const u32x4 v = (t & 2u) ? u32x4{s.z, s.w, s.x, s.y} : s;
+                    uint8_t *const d = (arr ? pv : pc) + 16 * q;
+                    if (hi == 16)
+                        *reinterpret_cast<u32x4 *>(d) = v;
+                    else
+                        store_chunk_part(d, v, 0u, hi);
+                }
+            }
+        } else {
+            for (uint32_t q = (uint32_t)lane; 16 * q < stop; q += kWave) {
+                const int32_t o = (int32_t)(16 * q) - (int32_t)a + (int32_t)j0;  // record of the chunk's first byte
+                const uint32_t lo = q == 0 ? a : 0u;
+                const uint32_t hi = span - 16 * q < 16 ? span - 16 * q : 16u;
+#pragma unroll
+                for (int arr = 0; arr < 2; ++arr) {
+                    const u32x4 v = piece_gather(arr ? stv : stc, o);
+                    uint8_t *const d = (arr ? pv : pc) + 16 * q;
+                    if (lo == 0 && hi == 16) {
+                        *reinterpret_cast<u32x4 *>(d) = v;  // (non-temporal: +-0.2 %)
+                    } else {
+                        store_chunk_part(d, v, lo, hi);
+                    }
                 }
             }
         }
