@@ -205,11 +205,9 @@ __device__ __forceinline__ void publish_aggregate(uint64_t *status, uint32_t til
 // aggregates back to tile 0 -- in fewer round trips.
 // Must stay inlined: a call makes the callee open with s_waitcnt vmcnt(0),
 // which would drain the caller's in-flight prefetch loads before the look-back.
-// (publish = false: the exclusive prefix only, for waves that share a tile
-// whose inclusive prefix another wave publishes.)
 template <int G, int L = kWave, int S = 1>
 __device__ __forceinline__ uint64_t lookback_resolve(uint64_t *status, uint32_t tile, uint64_t agg,
-                                                  Ctrl *ctrl, bool publish = true)
+                                                  Ctrl *ctrl)
 {
     static_assert(L >= 1 && L <= kWave && (G == 1 || L == kWave), "window of L lanes x G granules");
     const int lane = threadIdx.x & (kWave - 1);
@@ -261,7 +259,7 @@ __device__ __forceinline__ uint64_t lookback_resolve(uint64_t *status, uint32_t 
             break;
         j -= (int64_t)L * G;
     }
-    if (publish && lane == 0)
+    if (lane == 0)
         granule_store(&status[(size_t)tile * S], kFlagP | (excl + agg));
     return excl;
 }

@@ -1806,273 +1806,6 @@ __global__ __launch_bounds__(kWdThreads) void rl_decode_wave_kernel(
     }
 }
 
-// ---- dense decode with the offsets pass folded in, one block behind ---------
-// The two-kernel dense decode reads the counts twice, the offsets pre-pass
-// (~0.18 ms per GiB of counts at the read ceiling) before any output. Here
-// the workgroups take blocks of kPdKT wave tiles per wave by ticket, and
-// ticket T does three things: it decodes block T - lag, sums the counts of
-// block T (loaded with the decode's own tile loads, one tile ahead, so the sum
-// rides in the shadow of the decode), and resolves block T - lag/2's inclusive
-// prefix by a decoupled look-back over the blocks' aggregates. Every wait is on
-// an earlier ticket (a block is decoded lag tickets after its sum and lag/2
-// after its prefix), so no workgroup waits on one that is not running, and in
-// steady state none waits at all: the look-back window is loaded at the start
-// of the ticket and checked after the block's decode.
-constexpr int kPdKT = 8;  // wave tiles per wave per block
-template <int RPL>
-__global__ __launch_bounds__(kWdThreads, 4) void rl_decode_piped_kernel(  // (2nd: 4 waves per SIMD, 128 VGPRs)
-    const uint8_t *__restrict__ counts, const uint8_t *__restrict__ values, uint64_t runs,
-    uint8_t *__restrict__ out, uint64_t n, uint64_t ntiles, uint32_t nblk, uint32_t lag, Ctrl *ctrl,
-    uint64_t *bst, uint64_t *wgr)
-{
-    constexpr int NW = kWdThreads / kWave;
-    static_assert(RPL % 16 == 0, "whole vectors per lane");
-    constexpr int NV = RPL / 16;     // count / value vectors per lane
-    constexpr int TR = kWave * RPL;  // runs per wave tile
-    __shared__ u32x4 s_val4[NW][TR / 16 + 2];  // +32 B: the permute window reads up to 19 bytes past a run
-    __shared__ u32x4 s_bm4[NW][kWdWords / 4 + 1];
-    __shared__ u32x4 s_pre4[NW][kWdWords / 4];
-    __shared__ uint64_t s_pfx[kPfxSlots];
-    __shared__ uint32_t s_tk[2];
-    __shared__ uint32_t s_wsum[2][NW];
-    const int tid = threadIdx.x;
-    const int lane = tid & (kWave - 1);
-    const int wave = tid / kWave;
-    {
-        static_assert(kWdThreads == 256, "one table entry per thread");
-        uint64_t e = 0;
-        uint32_t c = 0;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            c += (tid >> i) & 1;
-            e |= (uint64_t)c << (8 * i);
-        }
-        s_pfx[pfx_slot(tid)] = e;
-    }
-    if (tid == 0)
-        s_tk[0] = atomicAdd(&ctrl->ticket, 1u);
-    u32x4 *const sv4 = s_val4[wave];
-    const uint32_t *const sv32 = reinterpret_cast<const uint32_t *>(sv4);
-    u32x4 *const bm4 = s_bm4[wave];
-    uint32_t *const bm = reinterpret_cast<uint32_t *>(bm4);
-    u32x4 *const pre4 = s_pre4[wave];
-    const uint32_t *const pre = reinterpret_cast<const uint32_t *>(pre4);
-    if (lane < 2)
-        sv4[TR / 16 + lane] = u32x4{0u, 0u, 0u, 0u};
-    __syncthreads();
-    const uint32_t tickets = nblk + lag;
-    uint32_t T = s_tk[0];
-    uint32_t slot = 1;
-    for (;;) {
-        if (T >= tickets) {
-            // a fresh counter hands out tickets + gridDim.x tickets in all
-            if (T >= tickets + gridDim.x && tid == 0)
-                raise_error(ctrl, FLRL_E_ARG);
-            break;
-        }
-        if (tid == 0)  // the next ticket, read after this ticket's barrier
-            s_tk[slot] = atomicAdd(&ctrl->ticket, 1u);
-        const bool dec = T >= lag, sum = T < nblk;
-        const uint32_t D = T - lag;
-        // block D's output base: its exclusive prefix by a decoupled look-back
-        // over the blocks' aggregates (every wave resolves it; wave 0, which
-        // alone reads block D's status before it turns inclusive, publishes
-        // the inclusive prefix), and this wave's offset in block D -- both
-        // published lag tickets ago with block D's sum, the offsets in granules
-        // of their own: wgr[2D] = waves 1 and 2, wgr[2D+1] = wave 3 (flag and
-        // payload in one granule, so no fences)
-        uint64_t wb = 0;
-        if (dec) {
-            uint32_t spins = 0;
-            uint64_t *const og = &wgr[2 * (size_t)D + (wave == 3 ? 1 : 0)];
-            uint64_t a = wave == 0 ? granule_load(&bst[D]) : kFlagA;
-            uint64_t o = wave == 0 ? kFlagA : granule_load(og);
-            while ((a >> 62) == 0u || (o >> 62) == 0u) {
-                if (++spins > kSpinLimit) {
-                    if (lane == 0)
-                        raise_error(ctrl, FLRL_E_TIMEOUT);
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(1);
-                if ((a >> 62) == 0u)
-                    a = granule_load(&bst[D]);
-                if ((o >> 62) == 0u)
-                    o = granule_load(og);
-            }
-            const uint64_t agg = a & kPayload;  // block 0: published as its inclusive prefix
-            const uint64_t excl = lookback_resolve<1>(bst, D, agg, ctrl, wave == 0);
-            if (D + 1 == nblk && wave == 0 && lane == 0 && excl + agg != n)
-                raise_error(ctrl, FLRL_E_FORMAT);
-            const uint64_t wo = wave == 0 ? 0ull : (wave == 2 ? (o >> 30) & ((1ull << 30) - 1) : o & ((1ull << 30) - 1));
-            wb = excl + wo;
-        }
-        const uint64_t dt0 = ((uint64_t)D * NW + wave) * kPdKT;  // this wave's first decode tile
-        const uint64_t st0 = ((uint64_t)T * NW + wave) * kPdKT;  // and first summed tile
-        u32x4 cv[NV], vv[NV], sc[NV];
-        auto load_dec = [&](uint64_t t) {
-            const uint64_t r = t * TR + lane * RPL;
-            if ((t + 1) * TR <= runs) {
-#pragma unroll
-                for (int v = 0; v < NV; ++v) {
-                    cv[v] = *reinterpret_cast<const u32x4 *>(counts + r + 16 * v);
-                    vv[v] = *reinterpret_cast<const u32x4 *>(values + r + 16 * v);
-                }
-            } else {
-#pragma unroll
-                for (int v = 0; v < NV; ++v) {
-                    cv[v] = load16_clamped(counts, r + 16 * v, runs);
-                    vv[v] = load16_clamped(values, r + 16 * v, runs);
-                }
-            }
-        };
-        auto load_sum = [&](uint64_t t) {
-            const uint64_t r = t * TR + lane * RPL;
-            if ((t + 1) * TR <= runs) {
-#pragma unroll
-                for (int v = 0; v < NV; ++v)  // (plain: the decode re-reads them lag tickets later)
-                    sc[v] = *reinterpret_cast<const u32x4 *>(counts + r + 16 * v);
-            } else {
-#pragma unroll
-                for (int v = 0; v < NV; ++v)
-                    sc[v] = load16_clamped(counts, r + 16 * v, runs);
-            }
-        };
-        const bool dec0 = dec && dt0 < ntiles, sum0 = sum && st0 < ntiles;
-        if (dec0)
-            load_dec(dt0);
-        if (sum0)
-            load_sum(st0);
-        uint32_t lsum = 0, zacc = 0;
-        for (int k = 0; k < kPdKT; ++k) {
-            const uint64_t tile = dt0 + k, stile = st0 + k;
-            const bool dk = dec && tile < ntiles, sk = sum && stile < ntiles;
-            // the summed tile's counts: SWAR sums, zero counts flagged
-            if (sk) {
-                const bool slast = (stile + 1) * TR > runs;
-#pragma unroll
-                for (int v = 0; v < NV; ++v) {
-                    const uint32_t valid = slast ? valid16(stile * TR + lane * RPL + 16 * v, runs) : 16u;
-#pragma unroll
-                    for (int d = 0; d < 4; ++d) {
-                        const uint32_t x = mask_dword(sc[v][d], valid, d);
-                        lsum = __builtin_amdgcn_udot4(x, 0x01010101u, lsum, false);
-                        zacc |= mask_dword((x - 0x01010101u) & ~x & 0x80808080u, valid, d);
-                    }
-                }
-            }
-            if (!dk) {
-                if (sk && k + 1 < kPdKT && stile + 1 < ntiles)
-                    load_sum(stile + 1);
-                continue;
-            }
-            wave_lds_sync();  // the previous tile's readers of the values are done
-            u32x4 cc[NV];
-            uint32_t S = 0;
-            const bool last = (tile + 1) * TR > runs;
-#pragma unroll
-            for (int v = 0; v < NV; ++v) {
-                sv4[lane * NV + v] = vv[v];
-                cc[v] = cv[v];
-                if (last) {
-                    const uint32_t valid = valid16(tile * TR + lane * RPL + 16 * v, runs);
-#pragma unroll
-                    for (int d = 0; d < 4; ++d)
-                        cc[v][d] = mask_dword(cc[v][d], valid, d);
-                }
-#pragma unroll
-                for (int d = 0; d < 4; ++d)
-                    S = __builtin_amdgcn_udot4(cc[v][d], 0x01010101u, S, false);
-            }
-            if (k + 1 < kPdKT) {  // next tiles' loads in flight during this one
-                if (tile + 1 < ntiles)
-                    load_dec(tile + 1);
-                if (sk && stile + 1 < ntiles)
-                    load_sum(stile + 1);
-            }
-            const uint32_t inc = wave_incl_scan_u32(S);
-            const uint64_t base = wb, end = wb + (uint32_t)__builtin_amdgcn_readlane((int)inc, kWave - 1);
-            wb = end;
-            if (end <= n && base < end) {  // else empty, or malformed (flagged: zero counts, total != n)
-                const uint64_t g0 = base & ~15ull;
-                const uint32_t o = (uint32_t)(base - g0) + inc - S;
-                const uint32_t len = (uint32_t)(end - g0);
-                uint32_t starts_before = 0;
-                for (uint32_t w = 0; w < len; w += kWdWin) {
-                    bm4[lane] = u32x4{0u, 0u, 0u, 0u};
-                    wave_lds_sync();
-                    uint32_t p = o - w;
-                    if (len <= (uint32_t)kWdWin) {
-#pragma unroll
-                        for (int i = 0; i < RPL; ++i) {
-                            atomicOr(bm + __builtin_amdgcn_ubfe(p, 5, 27), 1u << (p & 31));
-                            p += (cc[i >> 4][(i >> 2) & 3] >> (8 * (i & 3))) & 0xFFu;
-                        }
-                    } else {
-#pragma unroll
-                        for (int i = 0; i < RPL; ++i) {
-                            if (p <= (uint32_t)kWdWin)
-                                atomicOr(bm + __builtin_amdgcn_ubfe(p, 5, 27), 1u << (p & 31));
-                            p += (cc[i >> 4][(i >> 2) & 3] >> (8 * (i & 3))) & 0xFFu;
-                        }
-                    }
-                    wave_lds_sync();
-                    const u32x4 wd = bm4[lane];
-                    const uint32_t p0 = __popc(wd[0]), p1 = __popc(wd[1]), p2 = __popc(wd[2]), p3 = __popc(wd[3]);
-                    const uint32_t tsum = p0 + p1 + p2 + p3;
-                    const uint32_t tinc = wave_incl_scan_u32(tsum);
-                    const uint32_t e0 = tinc - tsum;
-                    pre4[lane] = u32x4{e0, e0 + p0, e0 + p0 + p1, e0 + p0 + p1 + p2};
-                    const uint32_t wtot = (uint32_t)__builtin_amdgcn_readlane((int)tinc, kWave - 1);
-                    wave_lds_sync();
-                    const uint32_t wl = len - w < (uint32_t)kWdWin ? len - w : (uint32_t)kWdWin;
-                    const uint32_t nch = (wl + 15) / 16;
-                    for (uint32_t q = lane; q < nch; q += kWave) {
-                        const uint32_t gq = w + 16u * q;
-                        const u32x4 ov = rd_chunk(bm, pre, sv32, s_pfx, q, starts_before);
-                        const uint32_t b0 = (uint32_t)(base - g0);
-                        const uint32_t lo = gq < b0 ? b0 - gq : 0u;
-                        const uint32_t hi = gq + 16 > len ? len - gq : 16u;
-                        if (lo == 0 && hi == 16)
-                            *reinterpret_cast<u32x4 *>(out + g0 + gq) = ov;
-                        else
-                            store_chunk_part(out + g0 + gq, ov, lo, hi);
-                    }
-                    starts_before += wtot;
-                    wave_lds_sync();
-                }
-            }
-        }
-        if (zacc != 0)
-            raise_error(ctrl, FLRL_E_FORMAT);
-        const uint32_t par = slot ^ 1u;  // this ticket's s_wsum half (the next ticket writes the other)
-        if (sum) {
-            const uint32_t ws = wave_sum_u32(lsum);
-            if (lane == 0)
-                s_wsum[par][wave] = ws;
-        }
-        __syncthreads();  // s_wsum of this ticket, s_tk of the next
-        const uint32_t Tn = s_tk[slot];
-        slot ^= 1u;
-        if (wave == 0) {
-            if (sum) {
-                // block T: its waves' offsets, then its aggregate (block 0: its prefix)
-                const uint64_t w0 = s_wsum[par][0], w1 = s_wsum[par][1], w2 = s_wsum[par][2], w3 = s_wsum[par][3];
-                const uint64_t tot = w0 + w1 + w2 + w3;  // < 2^25: 32 tiles of 4096 runs of <= 255 bytes
-                if (lane == 0) {
-                    publish_aggregate(bst, T, tot);
-                    if (T == 0 && nblk == 1 && tot != n)
-                        raise_error(ctrl, FLRL_E_FORMAT);
-                } else if (lane == 1) {
-                    granule_store(&wgr[2 * (size_t)T], kFlagA | w0 | ((w0 + w1) << 30));
-                } else if (lane == 2) {
-                    granule_store(&wgr[2 * (size_t)T + 1], kFlagA | (w0 + w1 + w2));
-                }
-            }
-        }
-        T = Tn;
-    }
-}
-
 // [Ctrl][status: tiles, one 128-B line each] (zeroed per call)
 struct RlEncLayout {
     size_t tiles, zero, bytes;
@@ -2086,7 +1819,6 @@ struct RlEncLayout {
 
 struct RlDecLayout {
     size_t tiles, blocks, iters, zero, bytes;
-    size_t pblk = 0, pwpre = 0;  // piped dense decode: blocks, offset of the wave-offset granules
     // tile_base is sized for the finer (wave) tiles; `tiles` counts the tiles
     // of the decode chosen for (runs, n)
     explicit RlDecLayout(size_t runs, size_t n = 0)
@@ -2103,13 +1835,6 @@ struct RlDecLayout {
         // scratch for an upper bound of runs): bound blocks monotonically
         const size_t bmax = std::min(div_up(runs, (size_t)kRoRuns), (size_t)kMaxPrefixBlocks);
         bytes = sizeof(Ctrl) + round_up(bmax * 8, 16) + round_up((div_up(runs, (size_t)kWdRuns) + 1) * 8, 16);
-#if FLRL_RL_PIPED
-        if (dense) {  // [Ctrl][block status][2 wave-offset granules per block], all zeroed, within bytes
-            pblk = div_up(div_up(runs, (size_t)(kWave * 64)), (size_t)(kWdThreads / kWave * kPdKT));
-            pwpre = sizeof(Ctrl) + round_up(pblk * 8, 16);
-            zero = std::max(zero, pwpre + pblk * 16);
-        }
-#endif
     }
 };
 
@@ -2186,26 +1911,6 @@ extern "C" int flrl_rl_decode_device(const uint8_t *d_counts, const uint8_t *d_v
     uint64_t *status = reinterpret_cast<uint64_t *>(ctrl + 1);
     uint64_t *tile_base =
         reinterpret_cast<uint64_t *>(static_cast<uint8_t *>(d_scratch) + L.zero);
-#if FLRL_RL_PIPED
-    if (dense) {
-        // mean run <= kWdDenseMean bytes: blocks of wave tiles by ticket, the
-        // offsets folded in (rl_decode_piped_kernel)
-        const size_t tiles = div_up(runs, (size_t)(kWave * 64));
-        const uint32_t nblk = (uint32_t)L.pblk;
-        const size_t gmax = (size_t)wd_per_cu<64>() * (size_t)cu_count();
-        // a block is decoded lag tickets after its sum: a ticket's aggregate is
-        // out about one grid of tickets after it was taken
-        const uint32_t lag = (uint32_t)std::min(gmax + gmax / 4, (size_t)nblk);
-        const dim3 grid((uint32_t)std::min(gmax, (size_t)nblk + lag));
-        kernel_timing_begin(s);
-        hipLaunchKernelGGL(rl_decode_piped_kernel<64>, grid, dim3(kWdThreads), 0, s, d_counts, d_values,
-                           (uint64_t)runs, d_out, (uint64_t)n, (uint64_t)tiles, nblk, lag, ctrl, status,
-                           reinterpret_cast<uint64_t *>(static_cast<uint8_t *>(d_scratch) + L.pwpre));
-        kernel_timing_end(s);
-        FLRL_HIP(hipGetLastError());
-        return FLRL_OK;
-    }
-#endif
     if (dense) {
         // mean run <= kWdDenseMean bytes: one wave per tile of 64 x RPL runs
         const bool densest = n <= kWd64Mean * runs;
