@@ -214,6 +214,43 @@ def test_medium_density(maxrun):
     check(np.repeat(vals, lens)[:2_000_003])
 
 
+def _dense_sparse(pattern, seed):
+    """4 KiB sub-chunks (one wave's 64 lanes x 64 B) after the pattern: 'd' random
+    bytes (more records than the wave's staging: the piece emission), 'm' runs of
+    1..3 bytes (the staging overflows part-way), 's' runs of 20..40 bytes, 'h'
+    half a sub-chunk of random bytes then a 255-byte run."""
+    rng = np.random.default_rng(seed)
+    parts = []
+    for c in pattern:
+        if c == "d":
+            parts.append(rng.integers(0, 256, size=4096, dtype=np.uint8))
+        elif c == "h":
+            parts.append(rng.integers(0, 256, size=2048, dtype=np.uint8))
+            parts.append(np.full(255, rng.integers(0, 256), dtype=np.uint8))
+        else:
+            lo, hi = (1, 4) if c == "m" else (20, 41)
+            lens = rng.integers(lo, hi, size=4096)
+            vals = (np.cumsum(rng.integers(1, 255, size=lens.size)) % 256).astype(np.uint8)
+            parts.append(np.repeat(vals, lens)[:4096])
+    return np.concatenate(parts)
+
+
+@pytest.mark.parametrize("pattern", ["d", "dd", "ds", "sd", "dsd", "dmd", "ddddddddd", "sdddddddsd",
+                                     "hdhd", "dhs", "m" * 8 + "d" * 8, "d" * 40])
+@pytest.mark.parametrize("tail", [0, 1, 15, 17, 1000, 4095])
+def test_dense_pieces_carry(pattern, tail):
+    """Dense sub-chunks store whole 16-byte chunks and carry a part's last partial
+    chunk into the next part (RlWave::piece_flush): dense runs starting at the input's
+    first byte (its first head ends no run), switching to and from sparse sub-chunks
+    (the carry flushed before the staging is reused), crossing tiles, and ending
+    in partial sub-chunks; bit-exact against the oracle, round trip exact."""
+    a = _dense_sparse(pattern, len(pattern) * 7 + tail)
+    if tail:
+        a = np.concatenate([a, np.random.default_rng(tail).integers(0, 256, size=tail, dtype=np.uint8)])
+    check(a)
+    check(a[1:])  # every chunk alignment of the output shifted by one record
+
+
 def test_decode_offsets_rounds():
     # random bytes: ~72M runs, more than 1024 x 65536, so the decode pre-pass
     # runs two rounds per workgroup with a partial last workgroup
