@@ -1648,9 +1648,9 @@ constexpr uint64_t kWd64Mean = FLRL_RL_WD64_MEAN;
 constexpr int kWdWin = 8192;               // output bytes per window
 constexpr int kWdWords = kWdWin / 32;      // bitmap words per window (4 per lane)
 constexpr int kWdThreads = 256;
-// resident workgroups per CU (VGPR-bound: 6 at 32 runs per lane, 4 at 64)
+// resident workgroups per CU (VGPR-bound: 6 at 32 runs per lane, 5 at 64), also the launch bound
 template <int RPL>
-constexpr int wd_per_cu() { return RPL == 64 ? 4 : 6; }
+constexpr int wd_per_cu() { return RPL == 64 ? FLRL_RD_WD64_PER_CU : 6; }
 // inputs with a mean run of at most this many bytes take the wave decode
 // (against the 512-thread block decode, 1 GiB: runs of 1..16 -15 %, 1..24
 // equal, 1..32 +4 %)
@@ -1660,7 +1660,7 @@ static_assert(kWdWords == 4 * kWave, "one bitmap vector per lane");
 
 
 template <int RPL>
-__global__ __launch_bounds__(kWdThreads) void rl_decode_wave_kernel(
+__global__ __launch_bounds__(kWdThreads, wd_per_cu<RPL>()) void rl_decode_wave_kernel(
     const uint8_t *__restrict__ counts, const uint8_t *__restrict__ values, uint64_t runs,
     uint8_t *__restrict__ out, uint64_t n, const uint64_t *__restrict__ tile_base, uint64_t ntiles)
 {

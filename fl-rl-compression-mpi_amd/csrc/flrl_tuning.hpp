@@ -17,7 +17,8 @@
      defined(FLRL_RL_STAGE) || defined(FLRL_RL_WPS) || defined(FLRL_RD_NARROW_MEAN) || defined(FLRL_RL_RO_MAXB) ||          \
      defined(FLRL_RD_UNROLL) || defined(FLRL_HOST_WORKERS) || defined(FLRL_HOST_CHUNK) ||                \
      defined(FLRL_HOST_DIRECT) || defined(FLRL_HOST_PROFILE) || defined(FLRL_HOST_THP) || defined(FLRL_RL_WD64_MEAN) || defined(FLRL_RL_DENSE_MEAN) ||\
-     defined(FLRL_FL_STORE_SPLIT) || defined(FLRL_FL_STORE_SKIP) || defined(FLRL_RL_SUB) || defined(FLRL_FL_STATIC_W) || defined(FLRL_RL_PMC_NOLB))
+     defined(FLRL_FL_STORE_SPLIT) || defined(FLRL_FL_STORE_SKIP) || defined(FLRL_RL_SUB) || defined(FLRL_FL_STATIC_W) || defined(FLRL_RL_PMC_NOLB) || \
+     defined(FLRL_RD_WD64_PER_CU))
 #error "FLRL_* kernel overrides are for timing harnesses only (define FLRL_TUNING_BUILD)"
 #endif
 
@@ -62,6 +63,9 @@
 #endif
 #ifndef FLRL_FL_STATIC_W
 #define FLRL_FL_STATIC_W 0  // PMC/timing builds: FL encode tile offsets = tile x frames x W, no look-back (exact only when every frame has width W)
+#endif
+#ifndef FLRL_RD_WD64_PER_CU
+#define FLRL_RD_WD64_PER_CU 5  // wave decode, 64 runs per lane: workgroups per CU, launch bound and grid (5: 96 VGPRs; 1 GiB random bytes -1.4 %, 4 GiB -5 %, 256 MiB +0.9 % against 4 at 104; 6 spills)
 #endif
 #ifndef FLRL_RL_PMC_NOLB
 #define FLRL_RL_PMC_NOLB 0  // PMC builds: RL encode without its look-back (every tile at state (0, 0); output wrong)
