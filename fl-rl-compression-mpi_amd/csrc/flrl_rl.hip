@@ -1650,7 +1650,7 @@ constexpr int kWdWords = kWdWin / 32;      // bitmap words per window (4 per lan
 constexpr int kWdThreads = 256;
 // resident workgroups per CU (VGPR-bound: 6 at 32 runs per lane, 5 at 64), also the launch bound
 template <int RPL>
-constexpr int wd_per_cu() { return RPL == 64 ? FLRL_RD_WD64_PER_CU : 6; }
+constexpr int wd_per_cu() { return RPL == 64 ? FLRL_RD_WD64_PER_CU : FLRL_RD_WD32_PER_CU; }
 // inputs with a mean run of at most this many bytes take the wave decode
 // (against the 512-thread block decode, 1 GiB: runs of 1..16 -15 %, 1..24
 // equal, 1..32 +4 %)

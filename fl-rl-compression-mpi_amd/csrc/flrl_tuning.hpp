@@ -18,7 +18,7 @@
      defined(FLRL_RD_UNROLL) || defined(FLRL_HOST_WORKERS) || defined(FLRL_HOST_CHUNK) ||                \
      defined(FLRL_HOST_DIRECT) || defined(FLRL_HOST_PROFILE) || defined(FLRL_HOST_THP) || defined(FLRL_RL_WD64_MEAN) || defined(FLRL_RL_DENSE_MEAN) ||\
      defined(FLRL_FL_STORE_SPLIT) || defined(FLRL_FL_STORE_SKIP) || defined(FLRL_RL_SUB) || defined(FLRL_FL_STATIC_W) || defined(FLRL_RL_PMC_NOLB) || \
-     defined(FLRL_RD_WD64_PER_CU))
+     defined(FLRL_RD_WD64_PER_CU) || defined(FLRL_RD_WD32_PER_CU))
 #error "FLRL_* kernel overrides are for timing harnesses only (define FLRL_TUNING_BUILD)"
 #endif
 
@@ -66,6 +66,9 @@
 #endif
 #ifndef FLRL_RD_WD64_PER_CU
 #define FLRL_RD_WD64_PER_CU 5  // wave decode, 64 runs per lane: workgroups per CU, launch bound and grid (5: 96 VGPRs; 1 GiB random bytes -1.4 %, 4 GiB -5 %, 256 MiB +0.9 % against 4 at 104; 6 spills)
+#endif
+#ifndef FLRL_RD_WD32_PER_CU
+#define FLRL_RD_WD32_PER_CU 6  // wave decode, 32 runs per lane: workgroups per CU, launch bound and grid (7: 72 VGPRs, runs of 1..3 to 1..12 -0.1..+1 %)
 #endif
 #ifndef FLRL_RL_PMC_NOLB
 #define FLRL_RL_PMC_NOLB 0  // PMC builds: RL encode without its look-back (every tile at state (0, 0); output wrong)
