@@ -4,9 +4,12 @@ TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and
 bench.py's cpu_baseline leg as the parity checker / CPU baseline; never by the
 product path (libflrl.so, the CLI, the flrl Python binding).
 
-FL is pinned by the golden vectors of SURVEY.md §8(c) (tests/golden/); RL has no
-reference implementation and is pinned only by IMPLEMENTATION-PLAN.md's worked
-examples (RL parity partially unpinned).
+FL is pinned by the plan's frame-length-3 example (IMPLEMENTATION-PLAN.md:9-13)
+and checked against the golden vectors of SURVEY.md §8(c) (tests/golden/), which
+came from a stand-in build of fl-cpu and corroborate without pinning (FL parity
+partially unpinned beyond the plan example); RL has no reference implementation
+and is pinned only by IMPLEMENTATION-PLAN.md's worked examples (RL parity
+partially unpinned).
 """
 from __future__ import annotations
 

@@ -5,10 +5,11 @@
  * __graft_entry__.smoke() and bench.py's cpu_baseline leg may load it. The
  * product path (libflrl.so, the `compress` CLI) never links or calls it.
  *
- * Pinning: the FL restatement is checked against the golden vectors recorded in
- * SURVEY.md §8(c) (KATs + sha256 of the reference fl-cpu's own output files,
- * produced by compiling the unmodified reference CPU path in the survey
- * container) — see tests/golden/. RL has no reference implementation
+ * Pinning: the FL restatement is pinned by the plan's frame-length-3 example
+ * (IMPLEMENTATION-PLAN.md:9-13) and checked against the golden vectors recorded
+ * in SURVEY.md §8(c) (KATs + sha256 of fl-cpu output files from a survey-session
+ * build with stand-in MPI/NCCL headers: they corroborate the restatement but do
+ * not pin it; FL parity partially unpinned) — see tests/golden/. RL has no reference implementation
  * (SURVEY.md §0 item 2): RL parity is pinned only by the worked examples of
  * IMPLEMENTATION-PLAN.md:87-89,125,158-160 ("RL parity partially unpinned").
  */
