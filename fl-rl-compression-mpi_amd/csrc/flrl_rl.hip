@@ -1806,7 +1806,7 @@ __global__ __launch_bounds__(kWdThreads, wd_per_cu<RPL>()) void rl_decode_wave_k
     }
 }
 
-// [Ctrl][status: tiles, one 128-B line each] (zeroed per call)
+// [Ctrl][status: tiles, kRlStatusStride granules apart] (zeroed per call)
 struct RlEncLayout {
     size_t tiles, zero, bytes;
     explicit RlEncLayout(size_t n)
